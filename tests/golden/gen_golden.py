@@ -1,0 +1,387 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REFERENCE itself (build container only).
+
+Runs ``/root/reference/ratslam/{posecell_network,convolution,view_templates}.py``
+under Python 3 with the minimum shims needed to reproduce their Python-2
+behaviour, and with the reference's own OpenCL kernel text (rendered by its own
+``Convolution.set_text``) compiled as host C by gcc (``-ffp-contract=off``) in
+place of PyOpenCL.  Nothing from the reference is written to the repository:
+only the resulting arrays, as ``tests/golden/*.npz``.
+
+Shims (each is the smallest change that restores the Python-2 meaning):
+  * ``builtins.xrange`` -> range yielding ``Py2Int`` (``/`` floors like Py2 ints),
+    so ``build_diff_gaussian_set_2d`` (posecell_network.py:55-58) and
+    ``ViewTemplates.__init__`` (view_templates.py:44-54) see integer division;
+  * ``builtins.math``: numpy-1.x's ``from numpy import *`` exported ``math``;
+  * module ``max``/``min`` reset to builtins (numpy-2's star export shadows
+    them; numpy 1.x removed them from ``__all__``), posecell_network.py:98;
+  * ``ceil`` in posecell_network returns ``int`` for scalars (Py2-era numpy
+    accepted float buffer shapes, convolution.py:662-665);
+  * ``raise E, msg`` -> ``raise E if 1 else msg`` in convolution.py (syntax only);
+  * fake ``mako.template.Template`` (``${name}`` substitution) and fake
+    ``pyopencl`` whose ``Program.build`` compiles the kernel text with gcc and
+    runs each NDRange as a host triple loop.
+
+Usage: python tests/golden/gen_golden.py [--out tests/golden]
+"""
+import argparse
+import builtins
+import ctypes
+import hashlib
+import math
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+REF = '/root/reference/ratslam'
+
+
+# ----------------------------------------------------------------------------
+# Python-2 integer semantics
+# ----------------------------------------------------------------------------
+class Py2Int(int):
+    """int whose true division floors, like Python-2 int / int."""
+
+    def __truediv__(self, other):
+        if isinstance(other, int):
+            return Py2Int(int(self) // int(other))
+        return int(self) / other
+
+    def __rtruediv__(self, other):
+        if isinstance(other, int):
+            return Py2Int(int(other) // int(self))
+        return other / int(self)
+
+
+class Py2IntArray(np.ndarray):
+    """integer ndarray whose ``/`` floors (numpy under Python 2)."""
+
+    def __truediv__(self, other):
+        return np.floor_divide(self, other)
+
+
+def py2_xrange(*args):
+    return (Py2Int(v) for v in range(*args))
+
+
+# ----------------------------------------------------------------------------
+# Fake mako + pyopencl (kernel text compiled as host C)
+# ----------------------------------------------------------------------------
+class FakeTemplate:
+    def __init__(self, text, output_encoding=None, **kw):
+        self.text = text
+        self.enc = output_encoding
+
+    def render(self, **conf):
+        out = re.sub(r'\$\{(\w+)\}', lambda m: str(conf[m.group(1)]), self.text)
+        return out.encode(self.enc) if self.enc else out
+
+
+_LIB_CACHE = {}
+_BUILD_DIR = tempfile.mkdtemp(prefix='ratslam_ref_')
+_SIG_RE = re.compile(r'__kernel\s+void\s+(\w+)\s*\(([^)]*)\)', re.S)
+
+
+def _compile_kernels(text):
+    if isinstance(text, bytes):
+        text = text.decode()
+    key = hashlib.sha1(text.encode()).hexdigest()
+    if key in _LIB_CACHE:
+        return _LIB_CACHE[key]
+    body = text.replace('\\\n', ' ')
+    wrappers = []
+    kernels = {}
+    for name, params in _SIG_RE.findall(body):
+        plist = [p.strip() for p in params.replace('\n', ' ').split(',') if p.strip()]
+        args, names, kinds = [], [], []
+        for p in plist:
+            p = p.replace('__global', '').strip()
+            m = re.match(r'(.*?)(\w+)$', p)
+            ctype_s, pname = m.group(1).strip(), m.group(2)
+            args.append(f'{ctype_s} {pname}')
+            names.append(pname)
+            kinds.append('ptr' if '*' in ctype_s else 'int')
+        wrappers.append(
+            f'void run_{name}({", ".join(args)}, unsigned g0, unsigned g1, unsigned g2) {{\n'
+            f'  for (unsigned a = 0; a < g0; a++) for (unsigned b = 0; b < g1; b++)\n'
+            f'  for (unsigned c = 0; c < g2; c++) {{ __gid[0]=a; __gid[1]=b; __gid[2]=c;\n'
+            f'    {name}({", ".join(names)}); }}\n}}\n')
+        kernels[name] = kinds
+    prelude = ('static unsigned __gid[3];\n#define __kernel static\n#define __global\n'
+               '#define get_global_id(d) (__gid[d])\n')
+    src = os.path.join(_BUILD_DIR, f'k_{key}.c')
+    lib = os.path.join(_BUILD_DIR, f'k_{key}.so')
+    with open(src, 'w') as f:
+        f.write(prelude + body + '\n' + '\n'.join(wrappers))
+    subprocess.check_call(['gcc', '-O2', '-ffp-contract=off', '-shared', '-fPIC', '-w',
+                           '-o', lib, src])
+    handle = ctypes.CDLL(lib)
+    _LIB_CACHE[key] = (handle, kernels)
+    return _LIB_CACHE[key]
+
+
+class _Buffer:
+    def __init__(self, ctx, flags, size=None, hostbuf=None):
+        if hostbuf is not None:
+            self.data = np.frombuffer(np.ascontiguousarray(hostbuf).tobytes(), dtype=np.uint8).copy()
+        else:
+            self.data = np.zeros(int(size), dtype=np.uint8)
+
+
+class _Event:
+    def wait(self):
+        return None
+
+
+class _Kernel:
+    def __init__(self, fn, kinds):
+        self.fn, self.kinds = fn, kinds
+
+    def __call__(self, queue, gsize, lsize, *args):
+        cargs = []
+        for kind, a in zip(self.kinds, args):
+            if kind == 'ptr':
+                cargs.append(ctypes.c_void_p(a.data.ctypes.data))
+            else:
+                cargs.append(ctypes.c_int(int(a)))
+        g = list(gsize) + [1] * (3 - len(gsize))
+        self.fn(*cargs, ctypes.c_uint(g[0]), ctypes.c_uint(g[1]), ctypes.c_uint(g[2]))
+        return _Event()
+
+
+class _Program:
+    def __init__(self, ctx, text):
+        self.text = text
+
+    def build(self):
+        self.lib, self.kernels = _compile_kernels(self.text)
+        return self
+
+    def __getattr__(self, name):
+        if name in ('lib', 'kernels', 'text'):
+            raise AttributeError(name)
+        return _Kernel(getattr(self.lib, 'run_' + name), self.kernels[name])
+
+
+def _enqueue_read_buffer(queue, buf, out):
+    flat = out.reshape(-1).view(np.uint8)
+    flat[:] = buf.data[:flat.size]
+    return _Event()
+
+
+def install_fakes():
+    cl = types.ModuleType('pyopencl')
+    cl.create_some_context = lambda *a, **k: object()
+    cl.CommandQueue = lambda ctx, *a, **k: object()
+    cl.mem_flags = types.SimpleNamespace(READ_ONLY=1, WRITE_ONLY=2, READ_WRITE=4, COPY_HOST_PTR=8)
+    cl.Buffer = _Buffer
+    cl.Program = _Program
+    cl.enqueue_read_buffer = _enqueue_read_buffer
+    sys.modules['pyopencl'] = cl
+    mako = types.ModuleType('mako')
+    tmpl = types.ModuleType('mako.template')
+    tmpl.Template = FakeTemplate
+    mako.template = tmpl
+    sys.modules['mako'] = mako
+    sys.modules['mako.template'] = tmpl
+    builtins.xrange = py2_xrange
+    builtins.math = math
+
+
+def load_reference():
+    """Import the reference modules with the shims above."""
+    install_fakes()
+    src = open(os.path.join(REF, 'convolution.py')).read()
+    src = re.sub(r'raise\s+(\w+)\s*,', r'raise \1 if 1 else ', src)
+    conv = types.ModuleType('convolution')
+    conv.__file__ = os.path.join(REF, 'convolution.py')
+    exec(compile(src, conv.__file__, 'exec'), conv.__dict__)
+    sys.modules['convolution'] = conv
+    sys.path.insert(0, REF)
+    import posecell_network as pn   # noqa: E402
+    import view_templates as vt     # noqa: E402
+    pn.max, pn.min = builtins.max, builtins.min
+    vt.max, vt.min = builtins.max, builtins.min
+    pn.ceil = lambda x: int(np.ceil(x)) if np.ndim(x) == 0 else np.ceil(x)
+    vt.arange = lambda n: np.arange(n).view(Py2IntArray)
+    return pn, vt
+
+
+# ----------------------------------------------------------------------------
+# Scenarios
+# ----------------------------------------------------------------------------
+def coo(p):
+    idx = np.flatnonzero(p)
+    return idx.astype(np.int64), p.ravel()[idx]
+
+
+def run_posecell(pn, shape, odom, inject_loc=None):
+    net = pn.PoseCellNetwork(shape)
+    loc = inject_loc or tuple(int(math.floor(s / 2)) for s in shape)
+    net.inject(1, loc)
+    maxes, nnz, idxs, vals, totals = [], [], [], [], []
+    for v in odom:
+        net.update((float(v[0]), float(v[1])))
+        maxes.append(net.max_pc)
+        i, x = coo(net.posecells)
+        nnz.append(len(i))
+        idxs.append(i)
+        vals.append(x)
+    return {
+        'shape': np.array(shape, dtype=np.int64),
+        'inject': np.array(loc, dtype=np.int64),
+        'odom': np.asarray(odom, dtype=np.float64),
+        'max_pc': np.array(maxes, dtype=np.int64),
+        'nnz': np.array(nnz, dtype=np.int64),
+        'coo_idx': np.concatenate(idxs),
+        'coo_val': np.concatenate(vals),
+    }
+
+
+def gen_kernels(pn, out):
+    net = pn.PoseCellNetwork((16, 16, 8))
+    lut = net.filter_dict_2d
+    keys = sorted(lut.keys())
+    one_d = {o: net.diff_gaussian_offset_1d(pn.PC_E_SIGMA, pn.PC_I_SIGMA, size=7, origin=o)
+             for o in range(-4, 5)}
+    np.savez_compressed(
+        os.path.join(out, 'kernels.npz'),
+        kernel_3d=net.kernel_3d,
+        lut_keys=np.array(keys, dtype=np.int64),
+        lut_filters=np.stack([lut[k] for k in keys]),
+        f1d_origins=np.arange(-4, 5),
+        f1d=np.stack([one_d[o] for o in range(-4, 5)]),
+        f2d_origin0=net.diff_gaussian_offset_2d(pn.PC_E_SIGMA, pn.PC_I_SIGMA, shape=(7, 7), origin=(0, 0)),
+    )
+
+
+def gen_posecell(pn, out):
+    rng = np.random.default_rng(0)
+    cases = {}
+    # synthetic odometry; seeds 0..2 at 32x32x18
+    for seed in range(3):
+        r = np.random.default_rng(seed)
+        odom = np.stack([r.uniform(0, 0.6, 40), r.uniform(-0.15, 0.15, 40)], axis=1)
+        cases[f'pc32_s{seed}'] = run_posecell(pn, (32, 32, 18), odom)
+    r = np.random.default_rng(0)
+    odom = np.stack([r.uniform(0, 0.6, 12), r.uniform(-0.15, 0.15, 12)], axis=1)
+    cases['pc64_s0'] = run_posecell(pn, (64, 64, 36), odom)
+    # the ROS node's grid (ros_simulate.py:31), odometry at 10 Hz-scaled magnitudes
+    r = np.random.default_rng(3)
+    odom = np.stack([r.uniform(0, 0.3, 30), r.uniform(-0.3, 0.3, 30)], axis=1)
+    cases['pc_ros21'] = run_posecell(pn, (21, 21, 36), odom)
+    # simulate.py:36-41 scenario (vtrans 3 m, vrot pi/4 on steps 4..8) on its grid
+    data = np.zeros((40, 2))
+    data[:, 0] = 3
+    data[4:9, 1] = np.pi / 4
+    cases['pc_simulate'] = run_posecell(pn, (50, 50, 10), data)
+    # non-cubic grid, off-centre injection
+    r = np.random.default_rng(4)
+    odom = np.stack([r.uniform(0, 0.6, 20), r.uniform(-0.15, 0.15, 20)], axis=1)
+    cases['pc_ragged'] = run_posecell(pn, (24, 40, 12), odom, inject_loc=(3, 37, 11))
+    for name, c in cases.items():
+        np.savez_compressed(os.path.join(out, f'{name}.npz'), **c)
+    # the +0.5 LUT KeyError: vtrans = 0.1 m -> 0.5 cell
+    net = pn.PoseCellNetwork((32, 32, 18))
+    net.inject(1, (16, 16, 9))
+    try:
+        net.update((0.1, 0.0))
+        raised = ''
+    except KeyError as e:
+        raised = repr(e.args[0])
+    np.savez_compressed(os.path.join(out, 'pc_keyerror.npz'),
+                        shape=np.array((32, 32, 18)), odom=np.array([[0.1, 0.0]]),
+                        raised=np.array(raised))
+    del rng
+
+
+def gen_templates(vt, out):
+    # per-pair scores: uint8 (wrapping) and float (true SAD), H in {32, 64}
+    rng = np.random.default_rng(1)
+    pairs_u8, pairs_f = [], []
+    for h, w in ((64, 32), (32, 32), (24, 20)):
+        a = rng.integers(0, 256, size=(40, h, w), dtype=np.uint8)
+        b = rng.integers(0, 256, size=(40, h, w), dtype=np.uint8)
+        # half of the pairs: b is a shifted, one-sided-noisy copy of a
+        for i in range(20):
+            sh = int(rng.integers(-7, 8))
+            b[i] = np.clip(np.roll(a[i], sh, axis=0).astype(int) - rng.integers(0, 4, (h, w)), 0, 255)
+        s = np.array([vt.ViewTemplate(0, 0, 0, 0, a[i]).match(b[i]) for i in range(40)])
+        pairs_u8.append((a, b, s.astype(np.uint64)))
+        af, bf = a.astype(np.float64), b.astype(np.float64)
+        sf = np.array([vt.ViewTemplate(0, 0, 0, 0, af[i]).match(bf[i]) for i in range(40)])
+        pairs_f.append((af, bf, sf))
+    np.savez_compressed(
+        os.path.join(out, 'vt_pairs.npz'),
+        **{f'u8_{i}_a': p[0] for i, p in enumerate(pairs_u8)},
+        **{f'u8_{i}_b': p[1] for i, p in enumerate(pairs_u8)},
+        **{f'u8_{i}_score': p[2] for i, p in enumerate(pairs_u8)},
+        **{f'f64_{i}_score': p[2] for i, p in enumerate(pairs_f)},
+    )
+
+    # library evolution through the unmodified ViewTemplates.match (:63-75)
+    def trace(name, im, x_range, y_range, step, thr, n_queries, seed, max_shift):
+        r = np.random.default_rng(seed)
+        vts = vt.ViewTemplates(x_range=(x_range[0], x_range[1]), y_range=(y_range[0], y_range[1]),
+                               x_step=Py2Int(step), y_step=Py2Int(step),
+                               im_x=im, im_y=im, match_threshold=thr)
+        vts.shape = tuple(int(s) for s in vts.shape)
+        vts.mask = np.asarray(vts.mask, dtype=bool).view(np.ndarray)
+        # first sight of a base is stored as-is; later sights are shifted copies
+        # minus one-sided noise (no uint8 wrap at the true offset), some with
+        # heavy noise so scores straddle the threshold; 25 % fresh frames miss
+        bases = r.integers(0, 256, size=(max(4, n_queries // 6), im, im), dtype=np.uint8)
+        seen = set()
+        images = np.empty((n_queries, im, im), dtype=np.uint8)
+        for i in range(n_queries):
+            if r.random() < 0.75:
+                b = int(r.integers(0, len(bases)))
+                if b not in seen:
+                    images[i] = bases[b]
+                    seen.add(b)
+                    continue
+                sh = 2 * int(r.integers(-max_shift, max_shift + 1))  # even: keeps the subsample grid
+                amp = 4 if r.random() < 0.7 else int(r.integers(40, 80))
+                noisy = np.roll(bases[b], sh, axis=0).astype(int) - r.integers(0, amp, (im, im))
+                images[i] = np.clip(noisy, 0, 255).astype(np.uint8)
+            else:
+                images[i] = r.integers(0, 256, size=(im, im), dtype=np.uint8)
+        pcs = r.integers(0, 21, size=(n_queries, 3))
+        idx, count = [], []
+        for i in range(n_queries):
+            m = vts.match(images[i], int(pcs[i, 0]), int(pcs[i, 1]), int(pcs[i, 2]))
+            idx.append(m.get_index())
+            count.append(len(vts.templates))
+        np.savez_compressed(
+            os.path.join(out, f'{name}.npz'),
+            queries=np.stack([im_[vts.mask].reshape(vts.shape) for im_ in images]),
+            pcs=pcs, index=np.array(idx), count=np.array(count),
+            mask=vts.mask, shape=np.array(vts.shape),
+            params=np.array([x_range[0], x_range[1], y_range[0], y_range[1], step, step, im, im, thr]),
+            templates=np.stack([t.template for t in vts.templates]),
+            locations=np.array([t.location() for t in vts.templates]))
+
+    # ROS configuration (ros_simulate.py:32-40): 256x256 mono8, 32x32 templates
+    trace('vt_trace_ros', 256, (32, 96), (32, 96), 2, 45000, 200, 5, 7)
+    # bench geometry: 64x32 templates (x span 128, y span 64, step 2) from 160x160 frames
+    trace('vt_trace_64x32', 160, (16, 144), (16, 80), 2, 45000, 300, 6, 3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--out', default=os.path.dirname(os.path.abspath(__file__)))
+    args = ap.parse_args()
+    pn, vt = load_reference()
+    gen_kernels(pn, args.out)
+    gen_posecell(pn, args.out)
+    gen_templates(vt, args.out)
+    print('golden vectors written to', args.out)
+
+
+if __name__ == '__main__':
+    main()
