@@ -1,0 +1,180 @@
+/*
+ * ratslam_abi.h -- C ABI of libratslam_hip.so, the MI355X (gfx950) hot path of
+ * pyratslam: the pose-cell network step and the view-template matcher.
+ *
+ * Plain C types only (pointers + sizes); every entry point returns an int
+ * status (RS_OK == 0) and leaves a thread-local message in rs_last_error().
+ * Host buffers are caller-owned and copied during the call; device memory is
+ * owned by the handle.  A handle is not re-entrant: callers serialise calls on
+ * one handle (the Python wrapper holds a per-handle lock); distinct handles may
+ * be used from different threads concurrently (ros_simulate.py:103 vs :135).
+ *
+ * What each entry point replaces in the reference (/root/reference/ratslam):
+ *   rs_pc_create    PoseCellNetwork.__init__      posecell_network.py:24-48
+ *                   + Convolution(...)/set_params convolution.py:11-91
+ *   rs_pc_update    PoseCellNetwork.update        posecell_network.py:326-353
+ *                   (conv_im x3 + host inhibition/normalisation/clamps/argmax,
+ *                    convolution.py:404-511, posecell_network.py:336-351)
+ *   rs_pc_excite    update() steps 1-4 alone      posecell_network.py:336-345
+ *   rs_pc_run       a loop of update() calls      simulate.py:31-34, ros_simulate.py:134-137
+ *   rs_pc_inject    PoseCellNetwork.inject        posecell_network.py:322-324
+ *   rs_pc_get_max   PoseCellNetwork.get_pc_max    posecell_network.py:317-319
+ *   rs_pc_read/write  the .posecells ndarray      posecell_network.py:27, simulate.py:60,
+ *                                                 ros_simulate.py:140,145
+ *   rs_vt_create    ViewTemplates.__init__        view_templates.py:42-57 (device library)
+ *   rs_vt_add       templates.append(...)         view_templates.py:68-70
+ *   rs_vt_match     ViewTemplates.match           view_templates.py:63-75
+ *                   (scores = ViewTemplate.match  view_templates.py:16-28)
+ *   rs_vt_match_batch  a loop of ViewTemplates.match calls (exact sequential
+ *                   semantics incl. in-batch appends), or a frozen-library scan
+ *   rs_vt_read      ViewTemplate.template         view_templates.py:11
+ *   rs_comm_*, rs_vt_attach_comm  (new) RCCL sharding of the library over GPUs
+ */
+#ifndef RATSLAM_ABI_H
+#define RATSLAM_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the Python wrapper maps them to exceptions) */
+#define RS_OK           0
+#define RS_ERR_ARG      1   /* ValueError   (bad size / index / parameter)          */
+#define RS_ERR_TYPE     2   /* TypeError    (shape/dtype mismatch, convolution.py:578-611) */
+#define RS_ERR_LUT_KEY  3   /* KeyError     (filter LUT miss, posecell_network.py:249) */
+#define RS_ERR_HIP      4   /* RuntimeError (HIP runtime failure)                    */
+#define RS_ERR_RCCL     5   /* RuntimeError (RCCL failure)                           */
+#define RS_ERR_STATE    6   /* RuntimeError (handle misuse)                          */
+#define RS_ERR_NOMEM    7   /* MemoryError                                           */
+
+#define RS_PREC_F32 0
+#define RS_PREC_F64 1
+
+#define RS_FILTER_LEN 7     /* PC_E_DIM, posecell_network.py:12; convolution.py:40 */
+
+/* library version, e.g. 100 for 0.1.0 */
+int rs_version(void);
+/* thread-local description of the last error on this thread ("" if none) */
+const char* rs_last_error(void);
+/* number of visible HIP devices (0 if none / no driver) */
+int rs_device_count(void);
+
+/* ------------------------------------------------------------------------ */
+/* Pose-cell network                                                         */
+/* ------------------------------------------------------------------------ */
+typedef struct rs_pc rs_pc;
+
+typedef struct rs_pc_params {
+    int precision;              /* RS_PREC_F32 (default) or RS_PREC_F64          */
+    double global_inhibition;   /* PC_GLOBAL_INHIB = 0.2 (posecell_network.py:15) */
+    /* 3-D excitation kernel K = (ge x ge x ge - gi x gi x gi) * k_scale, the exact
+     * rank-2 form of diff_gaussian(order=3) (posecell_network.py:97-113). */
+    double ge[RS_FILTER_LEN];
+    double gi[RS_FILTER_LEN];
+    double k_scale;             /* 1 / |sum(ge^3 - gi^3)|                         */
+    /* table of 7x7 path-integration filters (posecell_network.py:47,50-59),
+     * row-major [nfilters][7][7], F[x][y] with x along the first grid axis */
+    int nfilters;
+    const double* xy_filters;
+} rs_pc_params;
+
+/* Per-step control computed on the host from the odometry exactly as
+ * path_integration does (posecell_network.py:253-308):
+ *   ox, oy [TH]  integer shifts of each theta layer       (:262-265)
+ *   fidx   [TH]  index into the xy filter table per layer  (:249,271)
+ *   zf     [7]   1-D theta filter                           (:304-309)
+ * Batched forms are laid out step-major: ox[n*TH], oy[n*TH], fidx[n*TH], zf[n*7]. */
+
+int rs_pc_create(int X, int Y, int TH, const rs_pc_params* params, int device, rs_pc** out);
+int rs_pc_destroy(rs_pc* h);
+int rs_pc_shape(const rs_pc* h, int* X, int* Y, int* TH);
+
+/* one full update(); out_xyz = argmax cell (first in C order), as max_pc */
+int rs_pc_update(rs_pc* h, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                 const double* zf, int32_t out_xyz[3]);
+/* n consecutive updates with one host round trip; out_xyz[n*3] (may be NULL) */
+int rs_pc_run(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+              const double* zf, int32_t* out_xyz);
+/* steps 1-4 of update() alone (excitation, global inhibition, normalisation):
+ * the state the reference leaves behind when path_integration raises KeyError */
+int rs_pc_excite(rs_pc* h);
+int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th);
+int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]);
+/* whole volume as float64, C order (X, Y, TH) -- the reference's .posecells */
+int rs_pc_read(rs_pc* h, double* host_xyth);
+int rs_pc_write(rs_pc* h, const double* host_xyth);
+/* sum of all cells (float64 accumulation) */
+int rs_pc_total(rs_pc* h, double* total);
+/* device time of the last rs_pc_run/rs_pc_update, milliseconds (HIP events) */
+int rs_pc_last_ms(rs_pc* h, double* ms);
+/* HIP-event time of each kernel of the last rs_pc_run, summed over its steps:
+ * ms[0] = excitation kernel, ms[1] = path-integration kernel (events recorded
+ * around every launch on the handle's stream; only when profiling is enabled) */
+int rs_pc_set_profiling(rs_pc* h, int enable);
+int rs_pc_kernel_ms(rs_pc* h, double ms[2]);
+
+/* ------------------------------------------------------------------------ */
+/* View templates                                                            */
+/* ------------------------------------------------------------------------ */
+typedef struct rs_vt rs_vt;
+
+/* H x W uint8 templates, row shift max_offset (ViewTemplate.max_offset = 8,
+ * view_templates.py:14), strict threshold match_threshold (:67).
+ * capacity = initial number of templates this rank can hold (grows by doubling). */
+int rs_vt_create(int H, int W, int max_offset, uint64_t match_threshold, int64_t capacity,
+                 int device, rs_vt** out);
+int rs_vt_destroy(rs_vt* h);
+/* global number of stored templates (over all ranks) */
+int rs_vt_count(const rs_vt* h, int64_t* count);
+/* append n templates unconditionally (indices count .. count+n-1) */
+int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index);
+/* read back template `index` (only on its owning rank: index % nranks == rank) */
+int rs_vt_read(rs_vt* h, int64_t index, uint8_t* out);
+
+#define RS_VT_FROZEN     0   /* score against the current library only, never append   */
+#define RS_VT_SEQUENTIAL 1   /* exactly nq successive ViewTemplates.match calls          */
+
+/* Match nq queries (each H x W uint8, already subsampled).
+ * best_score[i]: the minimum score (UINT64_MAX if the library was empty)
+ * best_index[i]: the index ViewTemplates.match returns (first argmin, or the
+ *                new template's index when is_new[i] = 1)
+ * is_new[i]:     1 if query i was appended as a new template                 */
+int rs_vt_match_batch(rs_vt* h, int nq, const uint8_t* queries, int mode,
+                      uint64_t* best_score, int64_t* best_index, uint8_t* is_new);
+/* single query, RS_VT_SEQUENTIAL semantics */
+int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* best_index,
+                int* is_new);
+/* all pair scores of nq queries vs templates [t0, t0+nt) (owning rank's slots only;
+ * nranks must be 1): scores[q*nt + t]  -- ViewTemplate.match per pair */
+int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t nt,
+                 uint64_t* scores);
+/* The two halves of rs_vt_match_batch, for callers that combine the per-rank
+ * keys themselves (any min-reduction over ranks; key = score << 32 | index,
+ * UINT64_MAX = no template):
+ *   rs_vt_scan_local  stages the queries and returns this rank's keys;
+ *   rs_vt_resolve     takes the global (min over ranks) keys of the staged
+ *                     queries and applies ViewTemplates.match semantics,
+ *                     appending the new templates this rank owns.            */
+int rs_vt_scan_local(rs_vt* h, int nq, const uint8_t* queries, uint64_t* local_keys);
+int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint64_t* best_score,
+                  int64_t* best_index, uint8_t* is_new);
+/* device time (ms) of the scan kernel in the last match call (HIP events) */
+int rs_vt_last_ms(rs_vt* h, double* ms);
+
+/* Multi-GPU: one process per GPU, library sharded round-robin (template g lives
+ * on rank g % nranks at slot g / nranks); per query the local first-argmin keys
+ * (score << 32 | g) are combined with one RCCL allreduce(min, uint64).        */
+#define RS_UNIQUE_ID_BYTES 128
+int rs_comm_unique_id(uint8_t id[RS_UNIQUE_ID_BYTES]);
+int rs_vt_attach_comm(rs_vt* h, int rank, int nranks, const uint8_t id[RS_UNIQUE_ID_BYTES]);
+/* shard without a communicator (the caller reduces keys between scan_local and resolve) */
+int rs_vt_set_shard(rs_vt* h, int rank, int nranks);
+int rs_vt_rank(const rs_vt* h, int* rank, int* nranks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RATSLAM_ABI_H */

@@ -1,0 +1,152 @@
+"""ctypes binding of libratslam_hip.so (declared in include/ratslam_abi.h).
+
+The library is loaded from this package directory only (built in-tree by
+``pyratslam_amd._build``).  There is no fallback: if the shared object is
+missing or no HIP device is visible, the drop-in classes raise.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libratslam_hip.so')
+
+RS_OK = 0
+RS_ERR_ARG = 1
+RS_ERR_TYPE = 2
+RS_ERR_LUT_KEY = 3
+RS_ERR_HIP = 4
+RS_ERR_RCCL = 5
+RS_ERR_STATE = 6
+RS_ERR_NOMEM = 7
+RS_PREC_F32 = 0
+RS_PREC_F64 = 1
+RS_VT_FROZEN = 0
+RS_VT_SEQUENTIAL = 1
+RS_UNIQUE_ID_BYTES = 128
+FILTER_LEN = 7
+
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+
+
+class PcParams(ctypes.Structure):
+    """``rs_pc_params`` (ratslam_abi.h)."""
+    _fields_ = [
+        ('precision', ctypes.c_int),
+        ('global_inhibition', ctypes.c_double),
+        ('ge', ctypes.c_double * FILTER_LEN),
+        ('gi', ctypes.c_double * FILTER_LEN),
+        ('k_scale', ctypes.c_double),
+        ('nfilters', ctypes.c_int),
+        ('xy_filters', _f64p),
+    ]
+
+
+# name -> (restype, argtypes); every exported symbol of ratslam_abi.h
+SIGNATURES = {
+    'rs_version': (ctypes.c_int, []),
+    'rs_last_error': (ctypes.c_char_p, []),
+    'rs_device_count': (ctypes.c_int, []),
+    'rs_pc_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(PcParams), ctypes.c_int, ctypes.POINTER(_vp)]),
+    'rs_pc_destroy': (ctypes.c_int, [_vp]),
+    'rs_pc_shape': (ctypes.c_int, [_vp, _c_int_p, _c_int_p, _c_int_p]),
+    'rs_pc_update': (ctypes.c_int, [_vp, _i32p, _i32p, _i32p, _f64p, _i32p]),
+    'rs_pc_run': (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _i32p, _f64p, _i32p]),
+    'rs_pc_excite': (ctypes.c_int, [_vp]),
+    'rs_pc_inject': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    'rs_pc_get_max': (ctypes.c_int, [_vp, _i32p]),
+    'rs_pc_read': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_write': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_total': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_last_ms': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_set_profiling': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'rs_pc_kernel_ms': (ctypes.c_int, [_vp, _f64p]),
+    'rs_vt_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                    ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
+    'rs_vt_destroy': (ctypes.c_int, [_vp]),
+    'rs_vt_count': (ctypes.c_int, [_vp, _i64p]),
+    'rs_vt_add': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, _i64p]),
+    'rs_vt_read': (ctypes.c_int, [_vp, ctypes.c_int64, _u8p]),
+    'rs_vt_match_batch': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int, _u64p, _i64p, _u8p]),
+    'rs_vt_match': (ctypes.c_int, [_vp, _u8p, _u64p, _i64p, _c_int_p]),
+    'rs_vt_scores': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int64, ctypes.c_int64, _u64p]),
+    'rs_vt_scan_local': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, _u64p]),
+    'rs_vt_resolve': (ctypes.c_int, [_vp, ctypes.c_int, _u64p, ctypes.c_int, _u64p, _i64p, _u8p]),
+    'rs_vt_last_ms': (ctypes.c_int, [_vp, _f64p]),
+    'rs_comm_unique_id': (ctypes.c_int, [_u8p]),
+    'rs_vt_attach_comm': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _u8p]),
+    'rs_vt_set_shard': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    'rs_vt_rank': (ctypes.c_int, [_vp, _c_int_p, _c_int_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class HipLibraryError(RuntimeError):
+    """The HIP library is missing, failed to load, or reported a runtime error."""
+
+
+def load(path=LIB_PATH):
+    """Load (once) and return the ctypes handle; raises if the .so is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise HipLibraryError(
+                f'{path} not found: build it with `python -m pyratslam_amd._build` '
+                '(there is no CPU fallback)')
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(status):
+    """Map an rs_* status code to the exception the reference would raise."""
+    if status == RS_OK:
+        return
+    msg = (_lib.rs_last_error() or b'').decode(errors='replace') if _lib else ''
+    if status == RS_ERR_ARG:
+        raise ValueError(msg)
+    if status == RS_ERR_TYPE:
+        raise TypeError(msg)
+    if status == RS_ERR_LUT_KEY:
+        raise KeyError(msg)
+    if status == RS_ERR_NOMEM:
+        raise MemoryError(msg)
+    raise HipLibraryError(f'rs status {status}: {msg}')
+
+
+def require_device():
+    """Load the library and make sure a HIP device is visible."""
+    lib = load()
+    n = lib.rs_device_count()
+    if n <= 0:
+        raise HipLibraryError('no HIP device visible: the pyratslam_amd hot path runs only on '
+                              'an AMD GPU (gfx950); there is no CPU fallback')
+    return lib
+
+
+def ptr(a, ctype):
+    """ctypes pointer to a contiguous numpy array (None passes NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.POINTER(ctype))
+
+
+def as_c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)

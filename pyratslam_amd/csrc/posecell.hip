@@ -1,0 +1,864 @@
+// Pose-cell network step on MI355X (gfx950).
+//
+// Replaces PoseCellNetwork.update (/root/reference/ratslam/posecell_network.py:326-353)
+// and the three OpenCL kernels it drives through Convolution.conv_im
+// (convolution.py:228-246 `conv`, :320-340 `conv_xy_origin_filters`,
+// :344-359 `conv_z`) plus the host-side numpy passes between them.
+//
+// Device layout: the volume is stored layer-major, P[th][x][y] (y fastest), so
+// each theta layer -- the unit the path-integration shift acts on -- is one
+// contiguous periodic 2-D image.  The reference's C-order (x, y, th) appears
+// only at the boundary (rs_pc_read/write) and in the argmax tie-break index.
+//
+// One update() = two kernels on one stream:
+//   pc_excite : 3-D DoG excitation as the exact rank-2 separable form
+//               (ge^3 - gi^3)*scale, three 7-tap passes per Gaussian staged in
+//               LDS, fused with the global inhibition relu(v - 0.2) and a
+//               per-block float64 partial sum (normalisation total).
+//   pc_path   : sums the partials (-> total), per-layer shifted 7x7 filter
+//               (path integration), clamp, 7-tap theta filter, clamp, divide by
+//               total, write the new state, fused argmax (first max in the
+//               reference's C order) via a packed 64-bit atomicMax.
+// max(conv(Q/t), 0) == max(conv(Q), 0)/t for t > 0, so the normalisation is
+// applied once, at the end of the step.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "rs_common.h"
+
+namespace {
+
+constexpr int FL = RS_FILTER_LEN;  // 7 taps
+constexpr int HALF = FL / 2;       // 3
+constexpr int NT = 256;            // threads per block (4 waves)
+constexpr int FT = FL * FL;        // 49 taps of a 2-D filter
+
+template <typename T>
+struct SepKernel {
+    T ge[FL];
+    T gi[FL];
+    T scale;
+    T inhib;
+};
+
+// Tile shapes (output cells per block = BK layers x BX rows x BY cols).
+constexpr int EX_BX = 8, EX_BY = 16, EX_BK = 4;
+constexpr int PI_BX = 8, PI_BY = 16, PI_BK = 4;
+
+// Deterministic block sum of one double per thread (same value returned to all).
+__device__ inline double block_sum(double v, double* s_red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += s_red[i];
+    __syncthreads();
+    return t;
+}
+
+__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        unsigned long long o = __shfl_xor(v, off);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Packed argmax key for non-negative float values: larger value wins, then the
+// smaller reference linear index (numpy argmax returns the first maximum).
+__device__ inline unsigned long long argmax_key(float v, unsigned lin) {
+    return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 1: excitation (3-D DoG, separable) + global inhibition + partial sums
+// posecell_network.py:336-343 (conv -> inhibit -> sum)
+// ---------------------------------------------------------------------------
+template <typename T, int BX, int BY, int BK>
+__global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, T* __restrict__ Q,
+                                                        double* __restrict__ part,
+                                                        unsigned long long* __restrict__ res_slot,
+                                                        int X, int Y, int TH, SepKernel<T> k) {
+    constexpr int HX = BX + 2 * HALF, HY = BY + 2 * HALF, HK = BK + 2 * HALF;
+    __shared__ T s_in[HK * HX * HY];
+    __shared__ T s_ey[HK * HX * BY];
+    __shared__ T s_iy[HK * HX * BY];
+    __shared__ T s_exy[HK * BX * BY];
+    __shared__ T s_ixy[HK * BX * BY];
+    __shared__ double s_red[NT / 64];
+
+    const int tid = threadIdx.x;
+    const int j0 = blockIdx.x * BY, i0 = blockIdx.y * BX, k0 = blockIdx.z * BK;
+    if (res_slot != nullptr && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+        *res_slot = 0ull;  // the path kernel of this step max-reduces into it
+
+    for (int idx = tid; idx < HK * HX * HY; idx += NT) {
+        const int kk = idx / (HX * HY);
+        const int rem = idx - kk * (HX * HY);
+        const int a = rem / HY, b = rem - a * HY;
+        const int L = rs::wrapi(k0 - HALF + kk, TH);
+        const int r = rs::wrapi(i0 - HALF + a, X);
+        const int c = rs::wrapi(j0 - HALF + b, Y);
+        s_in[idx] = P[((size_t)L * X + r) * Y + c];
+    }
+    __syncthreads();
+
+    // pass along y (contiguous axis)
+    for (int idx = tid; idx < HK * HX * BY; idx += NT) {
+        const int row = idx / BY, j = idx - row * BY;
+        const T* src = s_in + row * HY + j;
+        T e = 0, g = 0;
+#pragma unroll
+        for (int t = 0; t < FL; ++t) {
+            const T v = src[t];
+            e += k.ge[t] * v;
+            g += k.gi[t] * v;
+        }
+        s_ey[idx] = e;
+        s_iy[idx] = g;
+    }
+    __syncthreads();
+
+    // pass along x
+    for (int idx = tid; idx < HK * BX * BY; idx += NT) {
+        const int kk = idx / (BX * BY);
+        const int rem = idx - kk * (BX * BY);
+        const int i = rem / BY, j = rem - i * BY;
+        const int base = (kk * HX + i) * BY + j;
+        T e = 0, g = 0;
+#pragma unroll
+        for (int t = 0; t < FL; ++t) {
+            e += k.ge[t] * s_ey[base + t * BY];
+            g += k.gi[t] * s_iy[base + t * BY];
+        }
+        s_exy[idx] = e;
+        s_ixy[idx] = g;
+    }
+    __syncthreads();
+
+    // pass along theta, then relu(v - inhib) (posecell_network.py:339-340)
+    double sum = 0.0;
+    for (int idx = tid; idx < BK * BX * BY; idx += NT) {
+        const int kq = idx / (BX * BY);
+        const int rem = idx - kq * (BX * BY);
+        const int i = rem / BY, j = rem - i * BY;
+        const int gk = k0 + kq, gi = i0 + i, gj = j0 + j;
+        if (gk < TH && gi < X && gj < Y) {
+            T e = 0, g = 0;
+#pragma unroll
+            for (int t = 0; t < FL; ++t) {
+                e += k.ge[t] * s_exy[idx + t * BX * BY];
+                g += k.gi[t] * s_ixy[idx + t * BX * BY];
+            }
+            const T v = (e - g) * k.scale;
+            const T q = (v < k.inhib) ? T(0) : v - k.inhib;
+            Q[((size_t)gk * X + gi) * Y + gj] = q;
+            sum += (double)q;
+        }
+    }
+    sum = block_sum(sum, s_red);
+    if (tid == 0) part[(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = sum;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: path integration (posecell_network.py:252-314) + normalisation
+// (:343-345, applied at the end) + argmax (:317-319)
+// ---------------------------------------------------------------------------
+template <typename T, int BX, int BY, int BK>
+__global__ __launch_bounds__(NT) void pc_path_kernel(
+    const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
+    const T* __restrict__ filt, const int* __restrict__ ctl_ox, const int* __restrict__ ctl_oy,
+    const int* __restrict__ ctl_f, const double* __restrict__ ctl_zf,
+    unsigned long long* __restrict__ res_slot, T* __restrict__ bmax, unsigned* __restrict__ bidx,
+    int X, int Y, int TH) {
+    constexpr int HX = BX + 2 * HALF, HY = BY + 2 * HALF, HK = BK + 2 * HALF;
+    __shared__ T s_win[HK * HX * HY];
+    __shared__ T s_r[HK * BX * BY];
+    __shared__ T s_f[HK * FT];
+    __shared__ int s_ox[HK], s_oy[HK];
+    __shared__ T s_zf[FL];
+    __shared__ double s_red[NT / 64];
+    __shared__ T s_bv[NT / 64];
+    __shared__ unsigned s_bl[NT / 64];
+
+    const int tid = threadIdx.x;
+    const int j0 = blockIdx.x * BY, i0 = blockIdx.y * BX, k0 = blockIdx.z * BK;
+
+    // normalisation total = sum of the excitation kernel's partials (fixed order)
+    double tot = 0.0;
+    for (int i = tid; i < npart; i += NT) tot += part[i];
+    tot = block_sum(tot, s_red);
+
+    if (tid < HK) {
+        const int L = rs::wrapi(k0 - HALF + tid, TH);
+        s_ox[tid] = ctl_ox[L];
+        s_oy[tid] = ctl_oy[L];
+    }
+    if (tid < FL) s_zf[tid] = (T)ctl_zf[tid];
+    for (int idx = tid; idx < HK * FT; idx += NT) {
+        const int kk = idx / FT, tap = idx - kk * FT;
+        const int L = rs::wrapi(k0 - HALF + kk, TH);
+        s_f[idx] = filt[ctl_f[L] * FT + tap];
+    }
+    __syncthreads();
+
+    // shifted window of every layer this tile (plus theta halo) needs
+    for (int idx = tid; idx < HK * HX * HY; idx += NT) {
+        const int kk = idx / (HX * HY);
+        const int rem = idx - kk * (HX * HY);
+        const int a = rem / HY, b = rem - a * HY;
+        const int L = rs::wrapi(k0 - HALF + kk, TH);
+        const int r = rs::wrapi(i0 - HALF + s_ox[kk] + a, X);
+        const int c = rs::wrapi(j0 - HALF + s_oy[kk] + b, Y);
+        s_win[idx] = Q[((size_t)L * X + r) * Y + c];
+    }
+    __syncthreads();
+
+    // per-layer 7x7 correlation with the layer's filter, clamp (:300)
+    for (int idx = tid; idx < HK * BX * BY; idx += NT) {
+        const int kk = idx / (BX * BY);
+        const int rem = idx - kk * (BX * BY);
+        const int i = rem / BY, j = rem - i * BY;
+        const T* w = s_win + (kk * HX + i) * HY + j;
+        const T* f = s_f + kk * FT;
+        T acc = 0;
+#pragma unroll
+        for (int x = 0; x < FL; ++x)
+#pragma unroll
+            for (int y = 0; y < FL; ++y) acc += w[x * HY + y] * f[x * FL + y];
+        s_r[idx] = acc > T(0) ? acc : T(0);
+    }
+    __syncthreads();
+
+    // theta filter, clamp (:310-314), normalise, store, argmax
+    unsigned long long best = 0ull;
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    const T tt = (T)tot;
+    for (int idx = tid; idx < BK * BX * BY; idx += NT) {
+        const int kq = idx / (BX * BY);
+        const int rem = idx - kq * (BX * BY);
+        const int i = rem / BY, j = rem - i * BY;
+        const int gk = k0 + kq, gi = i0 + i, gj = j0 + j;
+        if (gk < TH && gi < X && gj < Y) {
+            T acc = 0;
+#pragma unroll
+            for (int z = 0; z < FL; ++z) acc += s_r[idx + z * BX * BY] * s_zf[z];
+            T v = acc > T(0) ? acc : T(0);
+            if (tot != 0.0) v = v / tt;
+            P[((size_t)gk * X + gi) * Y + gj] = v;
+            const unsigned lin = ((unsigned)gi * Y + gj) * TH + gk;
+            if constexpr (sizeof(T) == 4) {
+                const unsigned long long key = argmax_key((float)v, lin);
+                best = key > best ? key : best;
+            } else {
+                if (v > bv || (v == bv && lin < bl)) {
+                    bv = v;
+                    bl = lin;
+                }
+            }
+        }
+    }
+    if constexpr (sizeof(T) == 4) {
+        best = wave_max_u64(best);
+        if ((tid & 63) == 0) atomicMax(res_slot, best);
+    } else {
+        // wave argmax, then block argmax, one (value, index) per block
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const T ov = __shfl_xor(bv, off);
+            const unsigned ol = __shfl_xor(bl, off);
+            if (ov > bv || (ov == bv && ol < bl)) {
+                bv = ov;
+                bl = ol;
+            }
+        }
+        if ((tid & 63) == 0) {
+            s_bv[tid >> 6] = bv;
+            s_bl[tid >> 6] = bl;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < NT / 64; ++w)
+                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                    bv = s_bv[w];
+                    bl = s_bl[w];
+                }
+            const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+            bmax[b] = bv;
+            bidx[b] = bl;
+        }
+    }
+}
+
+// One block reduces per-block (value, index) argmax partials into the packed slot.
+template <typename T>
+__global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ bmax,
+                                                         const unsigned* __restrict__ bidx, int nb,
+                                                         unsigned long long* __restrict__ res_slot) {
+    __shared__ T s_bv[NT];
+    __shared__ unsigned s_bl[NT];
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    for (int i = threadIdx.x; i < nb; i += NT) {
+        const T v = bmax[i];
+        const unsigned l = bidx[i];
+        if (v > bv || (v == bv && l < bl)) {
+            bv = v;
+            bl = l;
+        }
+    }
+    s_bv[threadIdx.x] = bv;
+    s_bl[threadIdx.x] = bl;
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            const T v = s_bv[threadIdx.x + s];
+            const unsigned l = s_bl[threadIdx.x + s];
+            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+                s_bv[threadIdx.x] = v;
+                s_bl[threadIdx.x] = l;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *res_slot = 0xFFFFFFFFull - s_bl[0];  // same decoding as the packed key
+}
+
+// Argmax of the stored state (get_pc_max outside update): per-block partials.
+template <typename T>
+__global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, int X, int Y, int TH,
+                                                       T* __restrict__ bmax,
+                                                       unsigned* __restrict__ bidx) {
+    __shared__ T s_bv[NT];
+    __shared__ unsigned s_bl[NT];
+    const size_t n = (size_t)X * Y * TH;
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    for (size_t e = blockIdx.x * (size_t)NT + threadIdx.x; e < n; e += (size_t)gridDim.x * NT) {
+        const int k = (int)(e / ((size_t)X * Y));
+        const int rem = (int)(e - (size_t)k * X * Y);
+        const int i = rem / Y, j = rem - i * Y;
+        const T v = P[e];
+        const unsigned lin = ((unsigned)i * Y + j) * TH + k;
+        if (v > bv || (v == bv && lin < bl)) {
+            bv = v;
+            bl = lin;
+        }
+    }
+    s_bv[threadIdx.x] = bv;
+    s_bl[threadIdx.x] = bl;
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) {
+            const T v = s_bv[threadIdx.x + s];
+            const unsigned l = s_bl[threadIdx.x + s];
+            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+                s_bv[threadIdx.x] = v;
+                s_bl[threadIdx.x] = l;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        bmax[blockIdx.x] = s_bv[0];
+        bidx[blockIdx.x] = s_bl[0];
+    }
+}
+
+template <typename T>
+__global__ void pc_export_kernel(const T* __restrict__ P, double* __restrict__ out, int X, int Y,
+                                 int TH) {
+    const size_t n = (size_t)X * Y * TH;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+         e += (size_t)gridDim.x * blockDim.x) {
+        // e indexes the C-order (x, y, th) output
+        const int k = (int)(e % TH);
+        const size_t xy = e / TH;
+        const int j = (int)(xy % Y), i = (int)(xy / Y);
+        out[e] = (double)P[((size_t)k * X + i) * Y + j];
+    }
+}
+
+template <typename T>
+__global__ void pc_import_kernel(const double* __restrict__ in, T* __restrict__ P, int X, int Y,
+                                 int TH) {
+    const size_t n = (size_t)X * Y * TH;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+         e += (size_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e % TH);
+        const size_t xy = e / TH;
+        const int j = (int)(xy % Y), i = (int)(xy / Y);
+        P[((size_t)k * X + i) * Y + j] = (T)in[e];
+    }
+}
+
+template <typename T>
+__global__ void pc_inject_kernel(T* __restrict__ P, size_t idx, double energy) {
+    if (threadIdx.x == 0) P[idx] = (T)((double)P[idx] + energy);
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void pc_total_kernel(const T* __restrict__ P, size_t n,
+                                                      double* __restrict__ out) {
+    __shared__ double s_red[NT / 64];
+    double s = 0.0;
+    for (size_t e = threadIdx.x; e < n; e += NT) s += (double)P[e];
+    s = block_sum(s, s_red);
+    if (threadIdx.x == 0) *out = s;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+struct rs_pc {
+    int X = 0, Y = 0, TH = 0, prec = RS_PREC_F32, device = 0;
+    size_t n = 0, esz = 4;
+    hipStream_t stream = nullptr;
+    void* dP = nullptr;
+    void* dQ = nullptr;
+    void* dFilt = nullptr;
+    int nf = 0;
+    double* dPart = nullptr;
+    int nPart = 0;               // blocks of the excitation kernel
+    int nPathBlocks = 0;         // blocks of the path kernel
+    void* dBmax = nullptr;       // f64 argmax partials (max(nPathBlocks, argmax grid))
+    unsigned* dBidx = nullptr;
+    int nBmaxCap = 0;
+    unsigned long long* dRes = nullptr;
+    int resCap = 0;
+    unsigned long long* hRes = nullptr;  // pinned
+    unsigned char* dCtl = nullptr;
+    unsigned char* hCtl = nullptr;       // pinned
+    size_t ctlStride = 0;
+    int ctlCap = 0;
+    double* dTmp = nullptr;              // export/import staging (n doubles)
+    double* dScalar = nullptr;
+    SepKernel<float> kf{};
+    SepKernel<double> kd{};
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float lastMs = 0.f;
+    bool profiling = false;
+    std::vector<hipEvent_t> evPool;
+    double kernelMs[2] = {0.0, 0.0};
+};
+
+namespace {
+
+int pc_grow_steps(rs_pc* h, int n) {
+    if (n <= h->ctlCap && n <= h->resCap) return RS_OK;
+    int cap = h->ctlCap > 0 ? h->ctlCap : 16;
+    while (cap < n) cap *= 2;
+    if (h->dCtl) RS_HIP(hipFree(h->dCtl));
+    if (h->hCtl) RS_HIP(hipHostFree(h->hCtl));
+    if (h->dRes) RS_HIP(hipFree(h->dRes));
+    if (h->hRes) RS_HIP(hipHostFree(h->hRes));
+    h->dCtl = nullptr; h->hCtl = nullptr; h->dRes = nullptr; h->hRes = nullptr;
+    RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
+    RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
+    RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * cap));
+    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap, hipHostMallocDefault));
+    h->ctlCap = cap;
+    h->resCap = cap;
+    return RS_OK;
+}
+
+int pc_ensure_events(rs_pc* h, size_t need) {
+    while (h->evPool.size() < need) {
+        hipEvent_t e;
+        RS_HIP(hipEventCreate(&e));
+        h->evPool.push_back(e);
+    }
+    return RS_OK;
+}
+
+// control record: int32 ox[TH] | int32 oy[TH] | int32 fidx[TH] | pad | double zf[8]
+inline size_t ctl_off_oy(const rs_pc* h) { return sizeof(int32_t) * h->TH; }
+inline size_t ctl_off_f(const rs_pc* h) { return 2 * sizeof(int32_t) * h->TH; }
+inline size_t ctl_off_zf(const rs_pc* h) { return rs::round_up(3 * sizeof(int32_t) * h->TH, 16); }
+
+int pc_pack_ctl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                const double* zf) {
+    RS_CHECK(ox && oy && fidx && zf, RS_ERR_ARG, "null control array");
+    const int TH = h->TH;
+    for (int s = 0; s < n; ++s) {
+        unsigned char* rec = h->hCtl + (size_t)s * h->ctlStride;
+        for (int k = 0; k < TH; ++k) {
+            const int32_t f = fidx[(size_t)s * TH + k];
+            RS_CHECK(f >= 0 && f < h->nf, RS_ERR_ARG,
+                     "step %d layer %d: filter index %d outside the table [0, %d)", s, k, f, h->nf);
+        }
+        std::memcpy(rec, ox + (size_t)s * TH, sizeof(int32_t) * TH);
+        std::memcpy(rec + ctl_off_oy(h), oy + (size_t)s * TH, sizeof(int32_t) * TH);
+        std::memcpy(rec + ctl_off_f(h), fidx + (size_t)s * TH, sizeof(int32_t) * TH);
+        std::memcpy(rec + ctl_off_zf(h), zf + (size_t)s * FL, sizeof(double) * FL);
+    }
+    return RS_OK;
+}
+
+template <typename T>
+const SepKernel<T>& sep_of(const rs_pc* h);
+template <>
+const SepKernel<float>& sep_of<float>(const rs_pc* h) { return h->kf; }
+template <>
+const SepKernel<double>& sep_of<double>(const rs_pc* h) { return h->kd; }
+
+template <typename T>
+int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
+    const T* P = static_cast<const T*>(h->dP);
+    T* Q = static_cast<T*>(h->dQ);
+    const SepKernel<T>& k = sep_of<T>(h);
+    unsigned long long* slot = h->dRes + s;
+    dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX, (h->TH + EX_BK - 1) / EX_BK);
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
+    hipLaunchKernelGGL((pc_excite_kernel<T, EX_BX, EX_BY, EX_BK>), gA, dim3(NT), 0, h->stream, P, Q,
+                       h->dPart, slot, h->X, h->Y, h->TH, k);
+    RS_HIP(hipGetLastError());
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+    if (excite_only) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
+    const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
+    dim3 gB((h->Y + PI_BY - 1) / PI_BY, (h->X + PI_BX - 1) / PI_BX, (h->TH + PI_BK - 1) / PI_BK);
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+    hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
+                       static_cast<T*>(h->dP), h->dPart, h->nPart,
+                       static_cast<const T*>(h->dFilt), reinterpret_cast<const int*>(rec),
+                       reinterpret_cast<const int*>(rec + ctl_off_oy(h)),
+                       reinterpret_cast<const int*>(rec + ctl_off_f(h)),
+                       reinterpret_cast<const double*>(rec + ctl_off_zf(h)), slot,
+                       static_cast<T*>(h->dBmax), h->dBidx, h->X, h->Y, h->TH);
+    RS_HIP(hipGetLastError());
+    if (sizeof(T) == 8) {
+        hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
+                           static_cast<const T*>(h->dBmax), h->dBidx, h->nPathBlocks, slot);
+        RS_HIP(hipGetLastError());
+    }
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 3], h->stream));
+    return RS_OK;
+}
+
+void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out) {
+    const unsigned lin = 0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull);
+    out[2] = (int32_t)(lin % (unsigned)h->TH);
+    const unsigned xy = lin / (unsigned)h->TH;
+    out[1] = (int32_t)(xy % (unsigned)h->Y);
+    out[0] = (int32_t)(xy / (unsigned)h->Y);
+}
+
+int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                const double* zf, int32_t* out_xyz) {
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(n >= 0, RS_ERR_ARG, "negative step count");
+    if (n == 0) return RS_OK;
+    RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_grow_steps(h, n));
+    RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
+    RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice, h->stream));
+    if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
+    RS_HIP(hipEventRecord(h->ev0, h->stream));
+    for (int s = 0; s < n; ++s) {
+        const int pb = h->profiling ? 4 * s : -1;
+        if (h->prec == RS_PREC_F32)
+            RS_TRY(pc_launch_step<float>(h, s, false, pb));
+        else
+            RS_TRY(pc_launch_step<double>(h, s, false, pb));
+    }
+    RS_HIP(hipEventRecord(h->ev1, h->stream));
+    RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost,
+                          h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    if (h->profiling) {
+        h->kernelMs[0] = h->kernelMs[1] = 0.0;
+        for (int s = 0; s < n; ++s) {
+            float a = 0.f, b = 0.f;
+            RS_HIP(hipEventElapsedTime(&a, h->evPool[4 * s], h->evPool[4 * s + 1]));
+            RS_HIP(hipEventElapsedTime(&b, h->evPool[4 * s + 2], h->evPool[4 * s + 3]));
+            h->kernelMs[0] += a;
+            h->kernelMs[1] += b;
+        }
+    }
+    if (out_xyz)
+        for (int s = 0; s < n; ++s) decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
+    return RS_OK;
+}
+
+template <typename T>
+int pc_argmax_impl(rs_pc* h, int32_t* out) {
+    const int nb = h->nBmaxCap < 1024 ? h->nBmaxCap : 1024;
+    hipLaunchKernelGGL((pc_argmax_blocks<T>), dim3(nb), dim3(NT), 0, h->stream,
+                       static_cast<const T*>(h->dP), h->X, h->Y, h->TH, static_cast<T*>(h->dBmax),
+                       h->dBidx);
+    RS_HIP(hipGetLastError());
+    hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
+                       static_cast<const T*>(h->dBmax), h->dBidx, nb, h->dRes);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    decode_xyz(h, h->hRes[0], out);
+    return RS_OK;
+}
+
+template <typename T>
+void fill_sep(SepKernel<T>& k, const rs_pc_params* p) {
+    for (int t = 0; t < FL; ++t) {
+        k.ge[t] = (T)p->ge[t];
+        k.gi[t] = (T)p->gi[t];
+    }
+    k.scale = (T)p->k_scale;
+    k.inhib = (T)p->global_inhibition;
+}
+
+// Scale the excited volume by 1/total in place (rs_pc_excite only).
+template <typename T>
+__global__ void pc_scale_kernel(T* __restrict__ P, size_t n, const double* __restrict__ part,
+                                int npart) {
+    __shared__ double s_red[NT / 64];
+    double t = 0.0;
+    for (int i = threadIdx.x; i < npart; i += NT) t += part[i];
+    t = block_sum(t, s_red);
+    if (t == 0.0) return;
+    const T tt = (T)t;
+    for (size_t e = blockIdx.x * (size_t)NT + threadIdx.x; e < n; e += (size_t)gridDim.x * NT)
+        P[e] = P[e] / tt;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// extern "C" entry points
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc** out) {
+    rs::clear_error();
+    RS_CHECK(out, RS_ERR_ARG, "null output handle pointer");
+    *out = nullptr;
+    RS_CHECK(p, RS_ERR_ARG, "null parameters");
+    RS_CHECK(X >= HALF && Y >= HALF && TH >= HALF, RS_ERR_ARG,
+             "grid (%d, %d, %d): every dimension must be >= %d (3-cell wrap halo, convolution.py:52-81)",
+             X, Y, TH, HALF);
+    RS_CHECK((size_t)X * Y * TH < 0xFFFFFFFFull, RS_ERR_ARG, "grid too large for 32-bit cell index");
+    RS_CHECK(p->precision == RS_PREC_F32 || p->precision == RS_PREC_F64, RS_ERR_ARG,
+             "precision must be RS_PREC_F32 or RS_PREC_F64");
+    RS_CHECK(p->nfilters >= 1 && p->xy_filters, RS_ERR_ARG, "empty path-integration filter table");
+    int ndev = 0;
+    RS_HIP(hipGetDeviceCount(&ndev));
+    RS_CHECK(device >= 0 && device < ndev, RS_ERR_ARG, "device %d not in [0, %d)", device, ndev);
+    RS_HIP(hipSetDevice(device));
+
+    rs_pc* h = new rs_pc();
+    h->X = X; h->Y = Y; h->TH = TH; h->prec = p->precision; h->device = device;
+    h->n = (size_t)X * Y * TH;
+    h->esz = p->precision == RS_PREC_F32 ? 4 : 8;
+    h->nf = p->nfilters;
+    fill_sep(h->kf, p);
+    fill_sep(h->kd, p);
+    h->ctlStride = rs::round_up(ctl_off_zf(h) + sizeof(double) * 8, 16);
+    h->nPart = ((Y + EX_BY - 1) / EX_BY) * ((X + EX_BX - 1) / EX_BX) * ((TH + EX_BK - 1) / EX_BK);
+    h->nPathBlocks =
+        ((Y + PI_BY - 1) / PI_BY) * ((X + PI_BX - 1) / PI_BX) * ((TH + PI_BK - 1) / PI_BK);
+    h->nBmaxCap = h->nPathBlocks > 1024 ? h->nPathBlocks : 1024;
+
+    auto fail = [&](int code) { rs_pc_destroy(h); return code; };
+    hipError_t e = hipSuccess;
+#define PC_ALLOC(call)                                                         \
+    do {                                                                       \
+        e = (call);                                                            \
+        if (e != hipSuccess) {                                                 \
+            rs::set_error("%s failed: %s", #call, hipGetErrorString(e));       \
+            return fail(e == hipErrorOutOfMemory ? RS_ERR_NOMEM : RS_ERR_HIP); \
+        }                                                                      \
+    } while (0)
+    PC_ALLOC(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    PC_ALLOC(hipMalloc(&h->dP, h->n * h->esz));
+    PC_ALLOC(hipMalloc(&h->dQ, h->n * h->esz));
+    PC_ALLOC(hipMemsetAsync(h->dP, 0, h->n * h->esz, h->stream));  // zeros(shape), :27
+    PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart));
+    PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
+    PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
+    PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
+    PC_ALLOC(hipMalloc(&h->dScalar, sizeof(double)));
+    PC_ALLOC(hipMalloc(&h->dFilt, h->esz * FT * h->nf));
+    if (h->prec == RS_PREC_F32) {
+        std::vector<float> f(FT * (size_t)h->nf);
+        for (size_t i = 0; i < f.size(); ++i) f[i] = (float)p->xy_filters[i];
+        PC_ALLOC(hipMemcpy(h->dFilt, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice));
+    } else {
+        PC_ALLOC(hipMemcpy(h->dFilt, p->xy_filters, FT * (size_t)h->nf * sizeof(double),
+                           hipMemcpyHostToDevice));
+    }
+    PC_ALLOC(hipEventCreate(&h->ev0));
+    PC_ALLOC(hipEventCreate(&h->ev1));
+#undef PC_ALLOC
+    int s = pc_grow_steps(h, 16);
+    if (s != RS_OK) return fail(s);
+    e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        rs::set_error("hipStreamSynchronize failed: %s", hipGetErrorString(e));
+        return fail(RS_ERR_HIP);
+    }
+    *out = h;
+    return RS_OK;
+}
+
+int rs_pc_destroy(rs_pc* h) {
+    if (!h) return RS_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx,
+                    (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
+        if (p) (void)hipFree(p);
+    if (h->hRes) (void)hipHostFree(h->hRes);
+    if (h->hCtl) (void)hipHostFree(h->hCtl);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    for (hipEvent_t e : h->evPool) (void)hipEventDestroy(e);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return RS_OK;
+}
+
+int rs_pc_shape(const rs_pc* h, int* X, int* Y, int* TH) {
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    if (X) *X = h->X;
+    if (Y) *Y = h->Y;
+    if (TH) *TH = h->TH;
+    return RS_OK;
+}
+
+int rs_pc_update(rs_pc* h, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                 const double* zf, int32_t out_xyz[3]) {
+    rs::clear_error();
+    return pc_run_impl(h, 1, ox, oy, fidx, zf, out_xyz);
+}
+
+int rs_pc_run(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+              const double* zf, int32_t* out_xyz) {
+    rs::clear_error();
+    return pc_run_impl(h, n, ox, oy, fidx, zf, out_xyz);
+}
+
+int rs_pc_excite(rs_pc* h) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_HIP(hipSetDevice(h->device));
+    if (h->prec == RS_PREC_F32) {
+        RS_TRY(pc_launch_step<float>(h, 0, true, -1));
+        hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
+                           static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
+    } else {
+        RS_TRY(pc_launch_step<double>(h, 0, true, -1));
+        hipLaunchKernelGGL((pc_scale_kernel<double>), dim3(64), dim3(NT), 0, h->stream,
+                           static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
+    }
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(x >= 0 && x < h->X && y >= 0 && y < h->Y && th >= 0 && th < h->TH, RS_ERR_ARG,
+             "inject location (%d, %d, %d) outside grid (%d, %d, %d)", x, y, th, h->X, h->Y, h->TH);
+    RS_HIP(hipSetDevice(h->device));
+    const size_t idx = ((size_t)th * h->X + x) * h->Y + y;
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_inject_kernel<float>), dim3(1), dim3(64), 0, h->stream,
+                           static_cast<float*>(h->dP), idx, energy);
+    else
+        hipLaunchKernelGGL((pc_inject_kernel<double>), dim3(1), dim3(64), 0, h->stream,
+                           static_cast<double*>(h->dP), idx, energy);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]) {
+    rs::clear_error();
+    RS_CHECK(h && out_xyz, RS_ERR_ARG, "null argument");
+    RS_HIP(hipSetDevice(h->device));
+    if (h->prec == RS_PREC_F32) return pc_argmax_impl<float>(h, out_xyz);
+    return pc_argmax_impl<double>(h, out_xyz);
+}
+
+int rs_pc_read(rs_pc* h, double* host) {
+    rs::clear_error();
+    RS_CHECK(h && host, RS_ERR_ARG, "null argument");
+    RS_HIP(hipSetDevice(h->device));
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_export_kernel<float>), dim3(256), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH);
+    else
+        hipLaunchKernelGGL((pc_export_kernel<double>), dim3(256), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_write(rs_pc* h, const double* host) {
+    rs::clear_error();
+    RS_CHECK(h && host, RS_ERR_ARG, "null argument");
+    RS_HIP(hipSetDevice(h->device));
+    RS_HIP(hipMemcpyAsync(h->dTmp, host, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_import_kernel<float>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
+                           static_cast<float*>(h->dP), h->X, h->Y, h->TH);
+    else
+        hipLaunchKernelGGL((pc_import_kernel<double>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
+                           static_cast<double*>(h->dP), h->X, h->Y, h->TH);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_total(rs_pc* h, double* total) {
+    rs::clear_error();
+    RS_CHECK(h && total, RS_ERR_ARG, "null argument");
+    RS_HIP(hipSetDevice(h->device));
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_total_kernel<float>), dim3(1), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), h->n, h->dScalar);
+    else
+        hipLaunchKernelGGL((pc_total_kernel<double>), dim3(1), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dP), h->n, h->dScalar);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipMemcpyAsync(total, h->dScalar, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_last_ms(rs_pc* h, double* ms) {
+    RS_CHECK(h && ms, RS_ERR_ARG, "null argument");
+    *ms = h->lastMs;
+    return RS_OK;
+}
+
+int rs_pc_set_profiling(rs_pc* h, int enable) {
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    h->profiling = enable != 0;
+    return RS_OK;
+}
+
+int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
+    RS_CHECK(h && ms, RS_ERR_ARG, "null argument");
+    ms[0] = h->kernelMs[0];
+    ms[1] = h->kernelMs[1];
+    return RS_OK;
+}
+
+}  // extern "C"

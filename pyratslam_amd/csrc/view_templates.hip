@@ -1,0 +1,820 @@
+// View-template matcher on MI355X (gfx950).
+//
+// Replaces ViewTemplate.match / ViewTemplates.match
+// (/root/reference/ratslam/view_templates.py:16-28, 63-75).
+//
+// Score of template T against query Q (both H x W uint8):
+//   min_{o=-(M-1)..M-1} sum_{r=M..H-M-1, c} (T[r+o][c] - Q[r][c]) mod 256
+// (numpy uint8 subtraction wraps and abs() is the identity on uint8).
+// Per 4-byte dword this is a carry-free SWAR add of the query's byte negation
+// c = -Q (mod 256):  d = ((a & 0x7f7f7f7f) + cL) ^ (a & 0x80808080) ^ cH, then
+// v_sad_u8(d, 0, acc) adds the four wrapped bytes: 3 VALU instructions
+// (v_add_u32, v_bitop3_b32 XOR3, v_sad_u8) per template-dword x offset pair.
+//
+// Library layout in HBM (SoA, 16-byte chunks): chunk (tb, c, q, t) at byte
+//   (((tb * WD + c) * HQ + q) * 64 + t) * 16
+// holds rows 4q..4q+3 (one dword each) of dword column c of template slot
+// tb*64 + t.  One global_load_dwordx4 by a wave = 1 KiB contiguous = the same
+// 16 bytes of 64 templates.
+//
+// Result of a scan: per query, the first argmin as a packed key
+// (score << 32) | global_index, min-reduced over lanes, waves and (RCCL
+// allreduce(min, uint64)) ranks -- exactly numpy's argmin tie-break
+// (view_templates.py:73).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "rs_common.h"
+
+namespace {
+
+constexpr int FAST_M = 8;  // ViewTemplate.max_offset (view_templates.py:14)
+constexpr unsigned long long NO_KEY = ~0ull;
+
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ inline uint32_t wrapped_pair(uint32_t aL, uint32_t aH, uint2 f, uint32_t acc) {
+    return __builtin_amdgcn_sad_u8(__builtin_amdgcn_bitop3_b32(aL + f.x, aH, f.y, 0x96), 0u, acc);
+}
+
+// Scatter n raw (H x W) templates into library slots (layout above).
+__global__ void vt_store_kernel(const uint8_t* __restrict__ raw, const int32_t* __restrict__ src,
+                                const int64_t* __restrict__ dst, int n, uint4* __restrict__ lib,
+                                int H, int W, int WD, int HQ) {
+    const int64_t total = (int64_t)n * WD * HQ;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int t = (int)(idx / (WD * HQ));
+        const int rem = (int)(idx - (int64_t)t * WD * HQ);
+        const int c = rem / HQ, q = rem - c * HQ;
+        const uint8_t* tpl = raw + (size_t)src[t] * H * W;
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int row = 4 * q + k;
+            uint32_t d = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int col = 4 * c + b;
+                const uint32_t byte = (row < H && col < W) ? tpl[(size_t)row * W + col] : 0u;
+                d |= byte << (8 * b);
+            }
+            w[k] = d;
+        }
+        const int64_t slot = dst[t];
+        const int64_t tb = slot >> 6, tl = slot & 63;
+        lib[((tb * WD + c) * HQ + q) * 64 + tl] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+// Query forms: qf[(n*WD + c)*H + r] = (cL, cH) of c = -Q[r][4c..4c+3] mod 256.
+__global__ void vt_qform_kernel(const uint8_t* __restrict__ raw, int n, int H, int W, int WD,
+                                uint2* __restrict__ qf) {
+    const int64_t total = (int64_t)n * WD * H;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int qn = (int)(idx / ((int64_t)WD * H));
+        const int rem = (int)(idx - (int64_t)qn * WD * H);
+        const int c = rem / H, r = rem - c * H;
+        uint32_t neg = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int col = 4 * c + b;
+            const uint32_t byte = col < W ? raw[((size_t)qn * H + r) * W + col] : 0u;
+            neg |= ((256u - byte) & 0xFFu) << (8 * b);
+        }
+        qf[idx] = make_uint2(neg & 0x7F7F7F7Fu, neg & 0x80808080u);
+    }
+}
+
+// Output of a scan: either min-reduce packed keys per query (best[]) or
+// write every (query, slot) score into a matrix.
+struct ScanOut {
+    unsigned long long* best;  // [nq] packed keys (MATRIX == false)
+    uint32_t* mat;             // [nq][ld]          (MATRIX == true)
+    int64_t ld;
+};
+
+template <bool MATRIX>
+__device__ inline void emit_score(const ScanOut& out, int64_t slot, int64_t count, int qi, int nq,
+                                  uint32_t score, int rank, int nranks, bool lane0_after_reduce) {
+    if constexpr (MATRIX) {
+        if (slot < count && qi < nq) out.mat[(size_t)qi * out.ld + slot] = score;
+    } else {
+        const unsigned long long g = (unsigned long long)slot * nranks + rank;
+        unsigned long long key = slot < count ? (((unsigned long long)score << 32) | g) : NO_KEY;
+        key = wave_min_u64(key);
+        if (lane0_after_reduce && qi < nq) atomicMin(out.best + qi, key);
+    }
+}
+
+// --- throughput form: one lane per template, 64 templates x NQ queries per wave.
+// Query forms are wave-uniform (scalar loads); each template dword is hoisted
+// once into (a & 0x7f7f7f7f, a & 0x80808080) and reused by the 2M-1 offsets.
+template <int H, int NQ, bool MATRIX>
+__global__ __launch_bounds__(64) void vt_scan_lane_kernel(const uint4* __restrict__ lib, int ntb,
+                                                          int64_t count, int WD,
+                                                          const uint2* __restrict__ qf, int nq,
+                                                          ScanOut out, int rank, int nranks) {
+    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
+    const int tb = blockIdx.x % ntb;
+    const int qbase = (blockIdx.x / ntb) * NQ;
+    const int lane = threadIdx.x;
+    uint32_t acc[NQ][NO];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
+
+    for (int c = 0; c < WD; ++c) {
+        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + lane;
+        uint32_t aL[4 * HQ], aH[4 * HQ];
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+            const uint4 v = col[(size_t)q * 64];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
+                aH[4 * q + k] = w[k] & 0x80808080u;
+            }
+        }
+#pragma unroll
+        for (int r = M; r < H - M; ++r) {
+#pragma unroll
+            for (int n = 0; n < NQ; ++n) {
+                const int qi = min(qbase + n, nq - 1);
+                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    const int s = r + o - (M - 1);
+                    acc[n][o] = wrapped_pair(aL[s], aH[s], f, acc[n][o]);
+                }
+            }
+        }
+    }
+    const int64_t slot = (int64_t)tb * 64 + lane;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+        uint32_t sc = acc[n][0];
+#pragma unroll
+        for (int o = 1; o < NO; ++o) sc = min(sc, acc[n][o]);
+        emit_score<MATRIX>(out, slot, count, qbase + n, nq, sc, rank, nranks, lane == 0);
+    }
+}
+
+// --- latency form: 8 lanes per template (one dword column each), 8 templates
+// per wave; the per-offset sums are combined across the 8 column lanes.
+template <int H, int NQ>
+__global__ __launch_bounds__(64) void vt_scan_col_kernel(const uint4* __restrict__ lib,
+                                                         int64_t count, int WD,
+                                                         const uint2* __restrict__ qf, int nq,
+                                                         ScanOut out, int rank, int nranks) {
+    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
+    const int lane = threadIdx.x;
+    const int t8 = lane >> 3, cl = lane & 7;
+    const int64_t slot = (int64_t)blockIdx.x * 8 + t8;
+    const int64_t tb = slot >> 6, tl = slot & 63;
+    const int qbase = blockIdx.y * NQ;
+    uint32_t acc[NQ][NO];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
+
+    for (int c = cl; c < WD; c += 8) {
+        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + tl;
+        uint32_t aL[4 * HQ], aH[4 * HQ];
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+            const uint4 v = col[(size_t)q * 64];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
+                aH[4 * q + k] = w[k] & 0x80808080u;
+            }
+        }
+#pragma unroll
+        for (int r = M; r < H - M; ++r) {
+#pragma unroll
+            for (int n = 0; n < NQ; ++n) {
+                const int qi = min(qbase + n, nq - 1);
+                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    const int s = r + o - (M - 1);
+                    acc[n][o] = wrapped_pair(aL[s], aH[s], f, acc[n][o]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+        uint32_t sc = 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            uint32_t v = acc[n][o];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            sc = min(sc, v);
+        }
+        const unsigned long long g = (unsigned long long)slot * nranks + rank;
+        unsigned long long key =
+            (slot < count && cl == 0) ? (((unsigned long long)sc << 32) | g) : NO_KEY;
+        key = wave_min_u64(key);
+        if (lane == 0 && qbase + n < nq) atomicMin(out.best + qbase + n, key);
+    }
+}
+
+// --- generic form (any H, max_offset): one thread per (slot, query).
+template <bool MATRIX>
+__global__ __launch_bounds__(64) void vt_scan_generic_kernel(const uint4* __restrict__ lib, int ntb,
+                                                             int64_t count, int H, int M, int WD,
+                                                             const uint2* __restrict__ qf, int nq,
+                                                             ScanOut out, int rank, int nranks) {
+    const int HQ = (H + 3) / 4;
+    const int tb = blockIdx.x % ntb;
+    const int qi = blockIdx.x / ntb;
+    const int lane = threadIdx.x;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(lib);
+    uint32_t best = 0xFFFFFFFFu;
+    bool any = false;
+    for (int o = -(M - 1); o <= M - 1; ++o) {
+        uint32_t acc = 0;
+        for (int r = M; r < H - M; ++r) {
+            const int s = r + o;
+            for (int c = 0; c < WD; ++c) {
+                const size_t chunk = ((size_t)(tb * WD + c) * HQ + (s >> 2)) * 64 + lane;
+                const uint32_t a = base[chunk * 4 + (s & 3)];
+                acc = wrapped_pair(a & 0x7F7F7F7Fu, a & 0x80808080u,
+                                   qf[((size_t)qi * WD + c) * H + r], acc);
+            }
+        }
+        best = min(best, acc);
+        any = true;
+    }
+    if (!any) best = 0;
+    emit_score<MATRIX>(out, (int64_t)tb * 64 + lane, count, qi, nq, best, rank, nranks, lane == 0);
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+struct rs_vt {
+    int H = 0, W = 0, M = 0, WD = 0, HQ = 0;
+    uint64_t thr = 0;
+    int device = 0;
+    int rank = 0, nranks = 1;
+    ncclComm_t comm = nullptr;
+    int64_t count = 0;     // global number of templates
+    int64_t localCap = 0;  // local slots allocated (multiple of 64)
+    uint4* dLib = nullptr;
+    hipStream_t stream = nullptr;
+    // query staging
+    int qCap = 0;
+    uint8_t* dQraw = nullptr;
+    uint8_t* hQraw = nullptr;  // pinned
+    uint2* dQf = nullptr;
+    unsigned long long* dBest = nullptr;
+    unsigned long long* hBest = nullptr;  // pinned
+    // index lists for stores
+    int idxCap = 0;
+    int32_t* dSrc = nullptr;
+    int64_t* dDst = nullptr;
+    int32_t* hSrc = nullptr;  // pinned
+    int64_t* hDst = nullptr;  // pinned
+    // candidate library and score matrix for in-batch resolution
+    int64_t candCap = 0;
+    uint4* dCand = nullptr;
+    size_t matCap = 0;
+    uint32_t* dMat = nullptr;
+    uint32_t* hMat = nullptr;  // pinned
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float lastMs = 0.f;
+    int stagedQ = 0;  // queries staged by the last scan
+};
+
+namespace {
+
+size_t tblock_bytes(const rs_vt* h) { return (size_t)h->WD * h->HQ * 64 * 16; }
+
+int64_t local_count_of(const rs_vt* h, int64_t global_count) {
+    if (global_count <= h->rank) return 0;
+    return (global_count - h->rank + h->nranks - 1) / h->nranks;
+}
+
+int vt_grow_lib(rs_vt* h, int64_t need_slots) {
+    if (need_slots <= h->localCap) return RS_OK;
+    int64_t cap = h->localCap > 0 ? h->localCap : 64;
+    while (cap < need_slots) cap *= 2;
+    cap = (int64_t)rs::round_up((size_t)cap, 64);
+    uint4* nl = nullptr;
+    const size_t bytes = (size_t)(cap / 64) * tblock_bytes(h);
+    hipError_t e = hipMalloc(&nl, bytes);
+    if (e != hipSuccess) {
+        rs::set_error("template library growth to %lld slots (%zu bytes) failed: %s",
+                      (long long)cap, bytes, hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? RS_ERR_NOMEM : RS_ERR_HIP;
+    }
+    RS_HIP(hipMemsetAsync(nl, 0, bytes, h->stream));
+    if (h->dLib) {
+        RS_HIP(hipMemcpyAsync(nl, h->dLib, (size_t)(h->localCap / 64) * tblock_bytes(h),
+                              hipMemcpyDeviceToDevice, h->stream));
+        RS_HIP(hipStreamSynchronize(h->stream));
+        RS_HIP(hipFree(h->dLib));
+    }
+    h->dLib = nl;
+    h->localCap = cap;
+    return RS_OK;
+}
+
+int vt_grow_queries(rs_vt* h, int nq) {
+    if (nq <= h->qCap) return RS_OK;
+    int cap = h->qCap > 0 ? h->qCap : 64;
+    while (cap < nq) cap *= 2;
+    if (h->dQraw) RS_HIP(hipFree(h->dQraw));
+    if (h->hQraw) RS_HIP(hipHostFree(h->hQraw));
+    if (h->dQf) RS_HIP(hipFree(h->dQf));
+    if (h->dBest) RS_HIP(hipFree(h->dBest));
+    if (h->hBest) RS_HIP(hipHostFree(h->hBest));
+    const size_t qb = (size_t)h->H * h->W;
+    RS_HIP(hipMalloc(&h->dQraw, qb * cap));
+    RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocDefault));
+    RS_HIP(hipMalloc(&h->dQf, sizeof(uint2) * (size_t)h->WD * h->H * cap));
+    RS_HIP(hipMalloc(&h->dBest, sizeof(unsigned long long) * cap));
+    RS_HIP(hipHostMalloc(&h->hBest, sizeof(unsigned long long) * cap, hipHostMallocDefault));
+    h->qCap = cap;
+    return RS_OK;
+}
+
+int vt_grow_index(rs_vt* h, int n) {
+    if (n <= h->idxCap) return RS_OK;
+    int cap = h->idxCap > 0 ? h->idxCap : 64;
+    while (cap < n) cap *= 2;
+    if (h->dSrc) RS_HIP(hipFree(h->dSrc));
+    if (h->dDst) RS_HIP(hipFree(h->dDst));
+    if (h->hSrc) RS_HIP(hipHostFree(h->hSrc));
+    if (h->hDst) RS_HIP(hipHostFree(h->hDst));
+    RS_HIP(hipMalloc(&h->dSrc, sizeof(int32_t) * cap));
+    RS_HIP(hipMalloc(&h->dDst, sizeof(int64_t) * cap));
+    RS_HIP(hipHostMalloc(&h->hSrc, sizeof(int32_t) * cap, hipHostMallocDefault));
+    RS_HIP(hipHostMalloc(&h->hDst, sizeof(int64_t) * cap, hipHostMallocDefault));
+    h->idxCap = cap;
+    return RS_OK;
+}
+
+int vt_grow_matrix(rs_vt* h, size_t elems) {
+    if (elems <= h->matCap) return RS_OK;
+    size_t cap = h->matCap > 0 ? h->matCap : 4096;
+    while (cap < elems) cap *= 2;
+    if (h->dMat) RS_HIP(hipFree(h->dMat));
+    if (h->hMat) RS_HIP(hipHostFree(h->hMat));
+    RS_HIP(hipMalloc(&h->dMat, sizeof(uint32_t) * cap));
+    RS_HIP(hipHostMalloc(&h->hMat, sizeof(uint32_t) * cap, hipHostMallocDefault));
+    h->matCap = cap;
+    return RS_OK;
+}
+
+int vt_grow_cand(rs_vt* h, int64_t slots) {
+    if (slots <= h->candCap) return RS_OK;
+    int64_t cap = h->candCap > 0 ? h->candCap : 64;
+    while (cap < slots) cap *= 2;
+    if (h->dCand) RS_HIP(hipFree(h->dCand));
+    RS_HIP(hipMalloc(&h->dCand, (size_t)(cap / 64) * tblock_bytes(h)));
+    h->candCap = cap;
+    return RS_OK;
+}
+
+// Upload nq raw queries and build their forms on the device.
+int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
+    RS_TRY(vt_grow_queries(h, nq));
+    const size_t qb = (size_t)h->H * h->W * nq;
+    std::memcpy(h->hQraw, queries, qb);
+    RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    const int64_t total = (int64_t)nq * h->WD * h->H;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(vt_qform_kernel, dim3(grid), dim3(256), 0, h->stream, h->dQraw, nq, h->H,
+                       h->W, h->WD, h->dQf);
+    RS_HIP(hipGetLastError());
+    return RS_OK;
+}
+
+// Store raw staged queries src[i] into slots dst[i] of `lib`.
+int vt_store(rs_vt* h, uint4* lib, const uint8_t* d_raw, int n) {
+    if (n == 0) return RS_OK;
+    RS_HIP(hipMemcpyAsync(h->dSrc, h->hSrc, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
+    RS_HIP(hipMemcpyAsync(h->dDst, h->hDst, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    const int64_t total = (int64_t)n * h->WD * h->HQ;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(vt_store_kernel, dim3(grid), dim3(256), 0, h->stream, d_raw, h->dSrc,
+                       h->dDst, n, lib, h->H, h->W, h->WD, h->HQ);
+    RS_HIP(hipGetLastError());
+    return RS_OK;
+}
+
+// Launch a scan of queries [0, nq) (forms in dQf) against `count` slots of lib.
+template <bool MATRIX>
+int vt_launch_scan(rs_vt* h, const uint4* lib, int64_t count, int nq, ScanOut out, int rank,
+                   int nranks) {
+    if (count <= 0 || nq <= 0) return RS_OK;
+    const int ntb = (int)((count + 63) / 64);
+    const bool fast = h->M == FAST_M && (h->H == 64 || h->H == 32);
+    RS_CHECK((int64_t)ntb * nq < (1ll << 31), RS_ERR_ARG, "scan grid too large (%d x %d)", ntb, nq);
+    if (fast && !MATRIX && (int64_t)ntb * nq < 2048 && h->WD <= 8) {
+        // few waves of work: spread each template over 8 column lanes
+        const int nb8 = (int)((count + 7) / 8);
+        if (h->H == 64)
+            hipLaunchKernelGGL((vt_scan_col_kernel<64, 1>), dim3(nb8, nq), dim3(64), 0, h->stream,
+                               lib, count, h->WD, h->dQf, nq, out, rank, nranks);
+        else
+            hipLaunchKernelGGL((vt_scan_col_kernel<32, 1>), dim3(nb8, nq), dim3(64), 0, h->stream,
+                               lib, count, h->WD, h->dQf, nq, out, rank, nranks);
+    } else if (fast) {
+        constexpr int NQ = 2;
+        const int nqg = (nq + NQ - 1) / NQ;
+        const dim3 grid((unsigned)(ntb * nqg));
+        if (h->H == 64)
+            hipLaunchKernelGGL((vt_scan_lane_kernel<64, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
+                               lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+        else
+            hipLaunchKernelGGL((vt_scan_lane_kernel<32, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
+                               lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+    } else {
+        hipLaunchKernelGGL((vt_scan_generic_kernel<MATRIX>), dim3((unsigned)(ntb * nq)), dim3(64),
+                           0, h->stream, lib, ntb, count, h->H, h->M, h->WD, h->dQf, nq, out, rank,
+                           nranks);
+    }
+    RS_HIP(hipGetLastError());
+    return RS_OK;
+}
+
+int vt_append_staged(rs_vt* h, const std::vector<std::pair<int, int64_t>>& news) {
+    // news: (staged query index, global index) in order
+    int mine = 0;
+    RS_TRY(vt_grow_index(h, (int)news.size() + 1));
+    const int64_t new_count = h->count + (int64_t)news.size();
+    RS_TRY(vt_grow_lib(h, local_count_of(h, new_count)));
+    for (const auto& p : news) {
+        if (p.second % h->nranks != h->rank) continue;
+        h->hSrc[mine] = p.first;
+        h->hDst[mine] = p.second / h->nranks;
+        ++mine;
+    }
+    RS_TRY(vt_store(h, h->dLib, h->dQraw, mine));
+    h->count = new_count;
+    return RS_OK;
+}
+
+// Stage nq queries and min-reduce their local first-argmin keys into dBest.
+int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries) {
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(nq >= 0, RS_ERR_ARG, "negative query count");
+    if (nq == 0) return RS_OK;
+    RS_CHECK(queries, RS_ERR_ARG, "null queries");
+    RS_HIP(hipSetDevice(h->device));
+    RS_TRY(vt_stage_queries(h, nq, queries));
+    RS_HIP(hipMemsetAsync(h->dBest, 0xFF, sizeof(unsigned long long) * nq, h->stream));
+    const int64_t lc = local_count_of(h, h->count);
+    ScanOut out{h->dBest, nullptr, 0};
+    RS_HIP(hipEventRecord(h->ev0, h->stream));
+    RS_TRY(vt_launch_scan<false>(h, h->dLib, lc, nq, out, h->rank, h->nranks));
+    RS_HIP(hipEventRecord(h->ev1, h->stream));
+    h->stagedQ = nq;
+    return RS_OK;
+}
+
+// Given the global keys of the staged queries, decide hits / new templates in
+// ViewTemplates.match order and append the new templates this rank owns.
+int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
+                    uint64_t* best_score, int64_t* best_index, uint8_t* is_new) {
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(mode == RS_VT_FROZEN || mode == RS_VT_SEQUENTIAL, RS_ERR_ARG, "unknown mode %d", mode);
+    RS_CHECK(nq == h->stagedQ, RS_ERR_STATE, "resolve of %d queries, %d staged", nq, h->stagedQ);
+    if (nq == 0) return RS_OK;
+    RS_CHECK(keys, RS_ERR_ARG, "null keys");
+    RS_HIP(hipSetDevice(h->device));
+    std::vector<unsigned long long> key(keys, keys + nq);
+    if (mode == RS_VT_FROZEN) {
+        for (int i = 0; i < nq; ++i) {
+            if (is_new) is_new[i] = 0;
+            if (best_index) best_index[i] = key[i] == NO_KEY ? -1 : (int64_t)(key[i] & 0xFFFFFFFFull);
+            if (best_score) best_score[i] = key[i] == NO_KEY ? UINT64_MAX : (key[i] >> 32);
+        }
+        return RS_OK;
+    }
+    // Candidates: queries that miss the stored library.  Only they can become
+    // templates; a later query may still prefer one of them (first argmin over
+    // the grown list, view_templates.py:65-73), so every candidate is scored as
+    // a template against every query once (replicated on all ranks).
+    std::vector<int> cand;
+    for (int i = 0; i < nq; ++i)
+        if (key[i] == NO_KEY || (key[i] >> 32) > h->thr) cand.push_back(i);
+    std::vector<int> cpos(nq, -1);
+    int64_t ldm = 0;
+    if (!cand.empty() && cand.front() < nq - 1) {
+        const int64_t C = (int64_t)cand.size();
+        RS_TRY(vt_grow_cand(h, (int64_t)rs::round_up((size_t)C, 64)));
+        RS_TRY(vt_grow_index(h, (int)C));
+        for (int64_t j = 0; j < C; ++j) {
+            h->hSrc[j] = cand[j];
+            h->hDst[j] = j;
+            cpos[cand[j]] = (int)j;
+        }
+        RS_TRY(vt_store(h, h->dCand, h->dQraw, (int)C));
+        ldm = (int64_t)rs::round_up((size_t)C, 64);
+        RS_TRY(vt_grow_matrix(h, (size_t)ldm * nq));
+        ScanOut mo{nullptr, h->dMat, ldm};
+        RS_TRY(vt_launch_scan<true>(h, h->dCand, C, nq, mo, 0, 1));
+        RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ldm * nq, hipMemcpyDeviceToHost,
+                              h->stream));
+        RS_HIP(hipStreamSynchronize(h->stream));
+    }
+    std::vector<std::pair<int, int64_t>> news;
+    for (int i = 0; i < nq; ++i) {
+        unsigned long long k = key[i];
+        for (size_t a = 0; a < news.size(); ++a) {
+            const int j = news[a].first;
+            const unsigned long long kj =
+                ((unsigned long long)h->hMat[(size_t)i * ldm + cpos[j]] << 32) |
+                (unsigned long long)news[a].second;
+            k = kj < k ? kj : k;
+        }
+        if (k == NO_KEY || (k >> 32) > h->thr) {
+            const int64_t g = h->count + (int64_t)news.size();
+            news.emplace_back(i, g);
+            if (is_new) is_new[i] = 1;
+            if (best_index) best_index[i] = g;
+        } else {
+            if (is_new) is_new[i] = 0;
+            if (best_index) best_index[i] = (int64_t)(k & 0xFFFFFFFFull);
+        }
+        if (best_score) best_score[i] = k == NO_KEY ? UINT64_MAX : (k >> 32);
+    }
+    RS_TRY(vt_append_staged(h, news));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
+    if (allreduce && h->nranks > 1) {
+        RS_CHECK(h->comm, RS_ERR_STATE, "sharded handle without a communicator: use "
+                 "rs_vt_scan_local + an external min-reduction + rs_vt_resolve");
+        ncclResult_t r = ncclAllReduce(h->dBest, h->dBest, (size_t)nq, ncclUint64, ncclMin, h->comm,
+                                       h->stream);
+        RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
+                 ncclGetErrorString(r));
+    }
+    RS_HIP(hipMemcpyAsync(h->hBest, h->dBest, sizeof(unsigned long long) * nq,
+                          hipMemcpyDeviceToHost, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    return RS_OK;
+}
+
+int vt_match_impl(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64_t* best_score,
+                  int64_t* best_index, uint8_t* is_new) {
+    RS_CHECK(mode == RS_VT_FROZEN || mode == RS_VT_SEQUENTIAL, RS_ERR_ARG, "unknown mode %d", mode);
+    RS_TRY(vt_scan_local_impl(h, nq, queries));
+    if (nq == 0) return RS_OK;
+    RS_TRY(vt_fetch_keys(h, nq, true));
+    return vt_resolve_impl(h, nq, h->hBest, mode, best_score, best_index, is_new);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, int device,
+                 rs_vt** out) {
+    rs::clear_error();
+    RS_CHECK(out, RS_ERR_ARG, "null output handle pointer");
+    *out = nullptr;
+    RS_CHECK(H > 0 && W > 0 && H <= 4096 && W <= 4096, RS_ERR_ARG, "bad template shape (%d, %d)", H, W);
+    RS_CHECK(max_offset >= 1 && max_offset <= 64, RS_ERR_ARG, "max_offset %d outside [1, 64]", max_offset);
+    RS_CHECK(capacity >= 0, RS_ERR_ARG, "negative capacity");
+    // max score H*W*255 must fit the 32-bit half of the packed key
+    RS_CHECK((uint64_t)H * W * 255u < 0xFFFFFFFFull, RS_ERR_ARG, "template too large");
+    int ndev = 0;
+    RS_HIP(hipGetDeviceCount(&ndev));
+    RS_CHECK(device >= 0 && device < ndev, RS_ERR_ARG, "device %d not in [0, %d)", device, ndev);
+    RS_HIP(hipSetDevice(device));
+    rs_vt* h = new rs_vt();
+    h->H = H; h->W = W; h->M = max_offset; h->thr = thr; h->device = device;
+    h->WD = (W + 3) / 4;
+    h->HQ = (H + 3) / 4;
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+    if (e != hipSuccess) {
+        rs::set_error("stream/event creation failed: %s", hipGetErrorString(e));
+        rs_vt_destroy(h);
+        return RS_ERR_HIP;
+    }
+    int s = vt_grow_lib(h, capacity > 0 ? capacity : 64);
+    if (s == RS_OK) s = vt_grow_queries(h, 64);
+    if (s == RS_OK) s = vt_grow_index(h, 64);
+    if (s != RS_OK) {
+        rs_vt_destroy(h);
+        return s;
+    }
+    *out = h;
+    return RS_OK;
+}
+
+int rs_vt_destroy(rs_vt* h) {
+    if (!h) return RS_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->comm) (void)ncclCommDestroy(h->comm);
+    for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dBest,
+                    (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat})
+        if (p) (void)hipFree(p);
+    for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat})
+        if (p) (void)hipHostFree(p);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return RS_OK;
+}
+
+int rs_vt_count(const rs_vt* h, int64_t* count) {
+    RS_CHECK(h && count, RS_ERR_ARG, "null argument");
+    *count = h->count;
+    return RS_OK;
+}
+
+int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(n >= 0 && (n == 0 || templates), RS_ERR_ARG, "bad template batch");
+    RS_HIP(hipSetDevice(h->device));
+    if (first_index) *first_index = h->count;
+    if (n == 0) return RS_OK;
+    RS_TRY(vt_grow_queries(h, n));
+    const size_t qb = (size_t)h->H * h->W * n;
+    std::memcpy(h->hQraw, templates, qb);
+    RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    std::vector<std::pair<int, int64_t>> news;
+    news.reserve(n);
+    for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
+    RS_TRY(vt_append_staged(h, news));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_vt_read(rs_vt* h, int64_t index, uint8_t* out) {
+    rs::clear_error();
+    RS_CHECK(h && out, RS_ERR_ARG, "null argument");
+    RS_CHECK(index >= 0 && index < h->count, RS_ERR_ARG, "template index %lld outside [0, %lld)",
+             (long long)index, (long long)h->count);
+    RS_CHECK(index % h->nranks == h->rank, RS_ERR_ARG, "template %lld lives on rank %lld",
+             (long long)index, (long long)(index % h->nranks));
+    RS_HIP(hipSetDevice(h->device));
+    const int64_t slot = index / h->nranks;
+    const int64_t tb = slot >> 6, tl = slot & 63;
+    std::vector<uint4> chunks((size_t)h->WD * h->HQ);
+    for (int c = 0; c < h->WD; ++c)
+        for (int q = 0; q < h->HQ; ++q)
+            RS_HIP(hipMemcpyAsync(&chunks[(size_t)c * h->HQ + q],
+                                  h->dLib + ((tb * h->WD + c) * h->HQ + q) * 64 + tl, sizeof(uint4),
+                                  hipMemcpyDeviceToHost, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    for (int r = 0; r < h->H; ++r)
+        for (int col = 0; col < h->W; ++col) {
+            const uint4& ch = chunks[(size_t)(col / 4) * h->HQ + r / 4];
+            const uint32_t w[4] = {ch.x, ch.y, ch.z, ch.w};
+            out[(size_t)r * h->W + col] = (uint8_t)(w[r & 3] >> (8 * (col & 3)));
+        }
+    return RS_OK;
+}
+
+int rs_vt_match_batch(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64_t* best_score,
+                      int64_t* best_index, uint8_t* is_new) {
+    rs::clear_error();
+    return vt_match_impl(h, nq, queries, mode, best_score, best_index, is_new);
+}
+
+int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* best_index,
+                int* is_new) {
+    rs::clear_error();
+    uint8_t nw = 0;
+    const int s = vt_match_impl(h, 1, query, RS_VT_SEQUENTIAL, best_score, best_index, &nw);
+    if (is_new) *is_new = nw;
+    return s;
+}
+
+int rs_vt_scan_local(rs_vt* h, int nq, const uint8_t* queries, uint64_t* local_keys) {
+    rs::clear_error();
+    RS_TRY(vt_scan_local_impl(h, nq, queries));
+    if (nq == 0) return RS_OK;
+    RS_TRY(vt_fetch_keys(h, nq, false));
+    if (local_keys) std::memcpy(local_keys, h->hBest, sizeof(uint64_t) * nq);
+    return RS_OK;
+}
+
+int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint64_t* best_score,
+                  int64_t* best_index, uint8_t* is_new) {
+    rs::clear_error();
+    static_assert(sizeof(uint64_t) == sizeof(unsigned long long), "key width");
+    return vt_resolve_impl(h, nq, reinterpret_cast<const unsigned long long*>(global_keys), mode,
+                           best_score, best_index, is_new);
+}
+
+int rs_vt_set_shard(rs_vt* h, int rank, int nranks) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, RS_ERR_ARG, "bad rank %d of %d", rank, nranks);
+    RS_CHECK(h->count == 0 && h->comm == nullptr, RS_ERR_STATE,
+             "set the shard before adding templates, once");
+    h->rank = rank;
+    h->nranks = nranks;
+    return RS_OK;
+}
+
+int rs_vt_rank(const rs_vt* h, int* rank, int* nranks) {
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    if (rank) *rank = h->rank;
+    if (nranks) *nranks = h->nranks;
+    return RS_OK;
+}
+
+int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t nt,
+                 uint64_t* scores) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(h->nranks == 1, RS_ERR_STATE, "rs_vt_scores needs an unsharded library");
+    RS_CHECK(nq >= 0 && t0 >= 0 && nt >= 0 && t0 + nt <= h->count, RS_ERR_ARG,
+             "template range [%lld, %lld) outside [0, %lld)", (long long)t0,
+             (long long)(t0 + nt), (long long)h->count);
+    if (nq == 0 || nt == 0) return RS_OK;
+    RS_CHECK(queries && scores, RS_ERR_ARG, "null argument");
+    RS_HIP(hipSetDevice(h->device));
+    RS_TRY(vt_stage_queries(h, nq, queries));
+    const int64_t ld = (int64_t)rs::round_up((size_t)h->count, 64);
+    RS_TRY(vt_grow_matrix(h, (size_t)ld * nq));
+    ScanOut mo{nullptr, h->dMat, ld};
+    RS_HIP(hipEventRecord(h->ev0, h->stream));
+    RS_TRY(vt_launch_scan<true>(h, h->dLib, h->count, nq, mo, 0, 1));
+    RS_HIP(hipEventRecord(h->ev1, h->stream));
+    RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ld * nq, hipMemcpyDeviceToHost,
+                          h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    for (int q = 0; q < nq; ++q)
+        for (int64_t t = 0; t < nt; ++t) scores[(size_t)q * nt + t] = h->hMat[(size_t)q * ld + t0 + t];
+    return RS_OK;
+}
+
+int rs_vt_last_ms(rs_vt* h, double* ms) {
+    RS_CHECK(h && ms, RS_ERR_ARG, "null argument");
+    *ms = h->lastMs;
+    return RS_OK;
+}
+
+int rs_comm_unique_id(uint8_t id[RS_UNIQUE_ID_BYTES]) {
+    rs::clear_error();
+    RS_CHECK(id, RS_ERR_ARG, "null id buffer");
+    static_assert(sizeof(ncclUniqueId) == RS_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    ncclResult_t r = ncclGetUniqueId(&u);
+    RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclGetUniqueId failed: %s", ncclGetErrorString(r));
+    std::memcpy(id, &u, sizeof(u));
+    return RS_OK;
+}
+
+int rs_vt_attach_comm(rs_vt* h, int rank, int nranks, const uint8_t id[RS_UNIQUE_ID_BYTES]) {
+    rs::clear_error();
+    RS_CHECK(h && id, RS_ERR_ARG, "null argument");
+    RS_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, RS_ERR_ARG, "bad rank %d of %d", rank, nranks);
+    RS_CHECK(h->count == 0 && h->comm == nullptr, RS_ERR_STATE,
+             "attach the communicator before adding templates, once");
+    RS_HIP(hipSetDevice(h->device));
+    if (nranks > 1) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        ncclResult_t r = ncclCommInitRank(&h->comm, nranks, u, rank);
+        RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
+    }
+    h->rank = rank;
+    h->nranks = nranks;
+    return RS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,179 @@
+"""Host-side filter construction and per-step control of the pose-cell network.
+
+These are the small host computations the reference performs in NumPy around
+its device kernels (``/root/reference/ratslam/posecell_network.py``).  They stay
+on the host, in NumPy/SciPy, so every control value handed to the GPU is
+bit-identical to the reference's: filter taps (``exp``/``cbrt`` on the same
+operands), the half-even ``around`` of the shifts, ``int`` truncation of the LUT
+key and ``floor(vrot + .5)``.  The GPU does all volume work.
+
+Semantics follow Python 2, the only interpreter the reference runs on
+(``convolution.py:25``): the LUT origins use integer division (:58).
+"""
+import math
+
+import numpy as np
+from scipy.special import cbrt
+
+# posecell_network.py:10-17
+PC_E_SIGMA = 1
+PC_I_SIGMA = 2
+PC_E_DIM = 7
+PC_I_DIM = 5
+PC_GLOBAL_INHIB = 0.2
+PC_CELL_X_SIZE = 0.2
+FILTER_LEN = 7
+LUT_PRECISION = 10          # filter_dict_2d_precision (:48)
+LUT_KEYS = range(-5, 5)     # xrange(-5*precision, 5*precision), precision = 1 (:55-56)
+
+_SQRT_2PI = math.sqrt(2 * math.pi)
+
+
+def _gauss_coef(sigma, order):
+    return 1.0 / (sigma * _SQRT_2PI) ** order
+
+
+def kernel_3d(dim_e=PC_E_DIM, dim_i=PC_I_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA):
+    """diff_gaussian(order=3) (posecell_network.py:97-113), bit-identical.
+
+    Every tap depends only on the integer squared radius d2 = dx^2+dy^2+dz^2, so
+    the 28 distinct values are evaluated with scalar ``math.exp`` (as the
+    reference does per tap) and scattered; the window masks are always 1 here.
+    """
+    dim = max(dim_e, dim_i)
+    c = dim // 2
+    d = np.arange(dim) - c
+    d2 = (d[:, None, None] ** 2 + d[None, :, None] ** 2 + d[None, None, :] ** 2)
+    ce, ci = _gauss_coef(sigma_e, 3), _gauss_coef(sigma_i, 3)
+    table = np.array([ce * math.exp(-r / (2 * sigma_e ** 2)) - ci * math.exp(-r / (2 * sigma_i ** 2))
+                      for r in range(int(d2.max()) + 1)])
+    k = table[d2]
+    k /= abs(np.sum(k.ravel()))
+    return k
+
+
+def separable_factors(dim=PC_E_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA):
+    """(ge, gi, scale) with kernel_3d == (ge x ge x ge - gi x gi x gi) * scale.
+
+    exp(-(dx^2+dy^2+dz^2)/2s^2)/(s*sqrt(2pi))^3 factorises exactly per axis, so the
+    343-tap kernel is rank 2 (agreement with kernel_3d ~2e-16).
+    """
+    d = np.arange(dim) - dim // 2
+    ge = np.exp(-(d ** 2) / (2.0 * sigma_e ** 2)) * _gauss_coef(sigma_e, 1)
+    gi = np.exp(-(d ** 2) / (2.0 * sigma_i ** 2)) * _gauss_coef(sigma_i, 1)
+    full = np.einsum('i,j,k->ijk', ge, ge, ge) - np.einsum('i,j,k->ijk', gi, gi, gi)
+    return ge, gi, 1.0 / abs(full.sum())
+
+
+def filter_2d(origin, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA, shape=(7, 7)):
+    """diff_gaussian_offset_2d (posecell_network.py:210-222), bit-identical.
+
+    'xy' meshgrid: the first origin component shifts the second array axis.
+    """
+    cols = np.arange(shape[0]) - origin[0] - shape[0] // 2
+    rows = np.arange(shape[1]) - origin[1] - shape[1] // 2
+    gx, gy = np.meshgrid(cols, rows)
+    neg_r2 = -gx ** 2 - gy ** 2
+    f = (1.0 / (2 * sigma_e ** 2 * np.pi)) * np.exp(neg_r2 / (2 * sigma_e ** 2)) - \
+        (1.0 / (2 * sigma_i ** 2 * np.pi)) * np.exp(neg_r2 / (2 * sigma_i ** 2))
+    f /= abs(np.sum(f.ravel()))
+    return cbrt(f)
+
+
+_F1D_CACHE = {}
+
+
+def filter_1d(origin, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA, size=7):
+    """diff_gaussian_offset_1d (posecell_network.py:224-235), bit-identical, memoised
+    per integer origin."""
+    key = (int(origin), sigma_e, sigma_i, size)
+    f = _F1D_CACHE.get(key)
+    if f is None:
+        sq = np.square(np.arange(size) - int(origin) - size // 2)
+        f = _gauss_coef(sigma_e, 1) * np.exp(-sq / (2 * sigma_e ** 2)) - \
+            _gauss_coef(sigma_i, 1) * np.exp(-sq / (2 * sigma_i ** 2))
+        f /= abs(np.sum(f.ravel()))
+        f = cbrt(f)
+        f.setflags(write=False)
+        _F1D_CACHE[key] = f
+    return f
+
+
+def lut_origin(key):
+    """Python-2 origin of LUT entry ``key`` (posecell_network.py:58): key // 10."""
+    return key // LUT_PRECISION
+
+
+class FilterTable:
+    """The 100-entry LUT ``filter_dict_2d`` (posecell_network.py:47,50-59) and the
+    table of its distinct filters uploaded to the device once."""
+
+    def __init__(self):
+        origins = sorted({(lut_origin(x), lut_origin(y)) for x in LUT_KEYS for y in LUT_KEYS})
+        self.origins = origins
+        self.index = {o: i for i, o in enumerate(origins)}
+        self.filters = np.stack([filter_2d(o) for o in origins])          # (nf, 7, 7)
+        self.dict = {(x, y): self.filters[self.index[(lut_origin(x), lut_origin(y))]]
+                     for x in LUT_KEYS for y in LUT_KEYS}
+        # key k (both components from the x residual, :249) -> table row, for k in [-5, 4]
+        self._key_to_row = np.array([self.index[(lut_origin(k), lut_origin(k))] for k in LUT_KEYS],
+                                    dtype=np.int32)
+
+    def rows_for_keys(self, keys):
+        """Table rows for per-layer keys; raises KeyError like posecell_network.py:249."""
+        keys = np.asarray(keys)
+        bad = (keys < LUT_KEYS.start) | (keys >= LUT_KEYS.stop)
+        if bad.any():
+            k = int(keys[np.argmax(bad)])
+            raise KeyError((k, k))
+        return self._key_to_row[keys - LUT_KEYS.start]
+
+
+def step_control(vtrans, vrot, th, table):
+    """Per-step control of path_integration (posecell_network.py:252-308).
+
+    Returns (ox, oy, rows, zf, radius) with ox/oy/rows int32[th], zf float64[7].
+    Same NumPy operations on the same operands as the reference, so bit-identical.
+    """
+    vrot_scale = 2.0 * np.pi / th
+    vt = vtrans / PC_CELL_X_SIZE
+    vr = vrot / vrot_scale
+    ang = (np.arange(th) - th // 2) * vrot_scale
+    ex = vt * np.cos(ang)
+    ey = vt * np.sin(ang)
+    rx = np.around(ex)
+    ry = np.around(ey)
+    keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)   # int() truncates
+    rows = table.rows_for_keys(keys)
+    zf = filter_1d(math.floor(vr + .5))
+    radius = int(np.ceil(abs(vt)))
+    return rx.astype(np.int32), ry.astype(np.int32), rows, zf, radius
+
+
+def batch_control(odometry, th, table):
+    """step_control for n steps at once (vectorised over steps).
+
+    Returns (ox, oy, rows, zf) shaped (n, th), (n, th), (n, th), (n, 7) and the
+    index of the first step whose LUT key is invalid (or None): steps before it
+    are valid, matching the point where the reference would raise.
+    """
+    od = np.asarray(odometry, dtype=np.float64).reshape(-1, 2)
+    n = od.shape[0]
+    vrot_scale = 2.0 * np.pi / th
+    vt = od[:, 0] / PC_CELL_X_SIZE
+    vr = od[:, 1] / vrot_scale
+    ang = (np.arange(th) - th // 2) * vrot_scale
+    ex = vt[:, None] * np.cos(ang)[None, :]
+    ey = vt[:, None] * np.sin(ang)[None, :]
+    rx = np.around(ex)
+    ry = np.around(ey)
+    keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)
+    bad = ((keys < LUT_KEYS.start) | (keys >= LUT_KEYS.stop)).any(axis=1)
+    first_bad = int(np.argmax(bad)) if bad.any() else None
+    keys = np.clip(keys, LUT_KEYS.start, LUT_KEYS.stop - 1)
+    rows = table._key_to_row[keys - LUT_KEYS.start]
+    zorig = np.floor(vr + .5).astype(np.int64)
+    zf = np.empty((n, FILTER_LEN))
+    for o in np.unique(zorig):
+        zf[zorig == o] = filter_1d(int(o))
+    return (rx.astype(np.int32), ry.astype(np.int32), rows.astype(np.int32), zf, first_bad)

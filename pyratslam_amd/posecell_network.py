@@ -1,0 +1,235 @@
+"""Drop-in ``PoseCellNetwork`` backed by the MI355X kernels of libratslam_hip.
+
+API of ``/root/reference/ratslam/posecell_network.py:22-353``: ``PoseCellNetwork(shape)``,
+``update(v)`` -> ``max_pc`` (also stored as ``.max_pc``), ``inject(energy, loc)``,
+``get_pc_max()``, ``.posecells`` (float64 ndarray, C order (X, Y, TH)), ``.shape``,
+plus the filter helpers the reference exposes.  ``step(v)`` is an alias of
+``update`` (the name BASELINE.json's north_star uses) and ``run(odometry)``
+performs many updates with one host round trip.
+
+The pose-cell volume lives on the GPU; ``.posecells`` copies it to the host
+on access (and uploads on assignment).  The per-step control scalars are
+derived on the host exactly as the reference derives them (``filters``), the
+volume work runs in ``pc_excite`` + ``pc_path`` (``csrc/posecell.hip``).
+"""
+import ctypes
+import math
+import threading
+
+import numpy as np
+
+from . import _lib
+from . import filters as F
+
+PC_DIM_XY = 21           # posecell_network.py:8 (unused by the reference too)
+PC_DIM_TH = 36
+PC_E_SIGMA = F.PC_E_SIGMA
+PC_I_SIGMA = F.PC_I_SIGMA
+PC_E_DIM = F.PC_E_DIM
+PC_I_DIM = F.PC_I_DIM
+PC_GLOBAL_INHIB = F.PC_GLOBAL_INHIB
+PC_CELL_X_SIZE = F.PC_CELL_X_SIZE
+PC_C_SIZE_TH = 2.0 * np.pi / PC_DIM_TH
+
+_PRECISIONS = {'float32': _lib.RS_PREC_F32, np.float32: _lib.RS_PREC_F32,
+               'float64': _lib.RS_PREC_F64, np.float64: _lib.RS_PREC_F64}
+
+
+def round_up(x):  # posecell_network.py:19-20
+    return math.ceil(x) if x > 0 else math.floor(x)
+
+
+class PoseCellNetwork:
+    """Continuous-attractor pose-cell network on one GPU.
+
+    ``precision``: 'float32' (default; activations within 1e-5 of the float64
+    reference) or 'float64'.  ``device``: HIP device ordinal.
+    Extra keyword arguments are accepted and ignored, like the reference (:24).
+    """
+
+    def __init__(self, shape, precision='float32', device=0, **kwargs):
+        if len(shape) != 3:
+            raise TypeError('PoseCellNetwork shape must be (X, Y, TH), got %r' % (shape,))
+        self.shape = tuple(int(s) for s in shape)
+        self.precision = 'float32' if _PRECISIONS[precision] == _lib.RS_PREC_F32 else 'float64'
+        self.device = int(device)
+        self.global_inhibition = PC_GLOBAL_INHIB
+        self.pc_vtrans_scale = PC_CELL_X_SIZE
+        self.pc_vrot_scale = 2.0 * np.pi / self.shape[2]
+        self.kernel_3d = F.kernel_3d()
+        self.filter_table = F.FilterTable()
+        self.filter_dict_2d = self.filter_table.dict
+        self.filter_dict_2d_precision = F.LUT_PRECISION
+        self.max_pc = None
+        self._max_valid = False
+        self._mutex = threading.Lock()
+        self._h = None
+        self._lib = _lib.require_device()
+        ge, gi, scale = F.separable_factors()
+        self._table = np.ascontiguousarray(self.filter_table.filters, dtype=np.float64)
+        params = _lib.PcParams()
+        params.precision = _PRECISIONS[precision]
+        params.global_inhibition = self.global_inhibition
+        params.ge[:] = list(ge)
+        params.gi[:] = list(gi)
+        params.k_scale = scale
+        params.nfilters = self._table.shape[0]
+        params.xy_filters = _lib.ptr(self._table, ctypes.c_double)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.rs_pc_create(*self.shape, ctypes.byref(params), self.device,
+                                          ctypes.byref(h)))
+        self._h = h
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if self._h is not None and self._h.value:
+            self._lib.rs_pc_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- state ------------------------------------------------------------------
+    @property
+    def posecells(self):
+        """Copy of the activity volume, float64 C order (X, Y, TH) (posecell_network.py:27)."""
+        out = np.empty(self.shape, dtype=np.float64)
+        with self._mutex:
+            _lib.check(self._lib.rs_pc_read(self._h, _lib.ptr(out, ctypes.c_double)))
+        return out
+
+    @posecells.setter
+    def posecells(self, value):
+        v = np.asarray(value)
+        if v.shape != self.shape:
+            raise TypeError('posecells must have shape %r, got %r' % (self.shape, v.shape))
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        with self._mutex:
+            _lib.check(self._lib.rs_pc_write(self._h, _lib.ptr(v, ctypes.c_double)))
+            self._max_valid = False
+
+    def total(self):
+        t = ctypes.c_double()
+        with self._mutex:
+            _lib.check(self._lib.rs_pc_total(self._h, ctypes.byref(t)))
+        return t.value
+
+    # -- reference API ----------------------------------------------------------
+    def inject(self, energy, loc):
+        """posecells[loc] += energy for one cell ``loc = (x, y, th)`` (posecell_network.py:322-324)."""
+        if isinstance(loc, list):
+            raise TypeError('inject expects a tuple (x, y, th); the reference would fancy-index '
+                            'whole planes with a list (posecell_network.py:324)')
+        x, y, th = (int(v) for v in loc)
+        X, Y, TH = self.shape
+        # numpy indexing semantics: negative indices count from the end
+        x, y, th = x + X if x < 0 else x, y + Y if y < 0 else y, th + TH if th < 0 else th
+        if not (0 <= x < X and 0 <= y < Y and 0 <= th < TH):
+            raise IndexError('inject location %r outside grid %r' % (loc, self.shape))
+        with self._mutex:
+            _lib.check(self._lib.rs_pc_inject(self._h, float(energy), x, y, th))
+            self._max_valid = False
+
+    def get_pc_max(self):
+        """Argmax cell (first maximum in C order) (posecell_network.py:317-319)."""
+        with self._mutex:
+            if self._max_valid:
+                return self.max_pc
+            out = np.empty(3, dtype=np.int32)
+            _lib.check(self._lib.rs_pc_get_max(self._h, _lib.ptr(out, ctypes.c_int32)))
+        return tuple(int(v) for v in out)
+
+    def update(self, v=(0.0, 0.0)):
+        """One network step (posecell_network.py:326-353); returns and stores max_pc."""
+        vtrans, vrot = float(v[0]), float(v[1])
+        try:
+            ox, oy, rows, zf, _ = F.step_control(vtrans, vrot, self.shape[2], self.filter_table)
+        except KeyError:
+            # the reference raises inside path_integration, after steps 1-4 ran
+            with self._mutex:
+                _lib.check(self._lib.rs_pc_excite(self._h))
+                self._max_valid = False
+            raise
+        out = np.empty(3, dtype=np.int32)
+        with self._mutex:
+            _lib.check(self._lib.rs_pc_update(
+                self._h, _lib.ptr(ox, ctypes.c_int32), _lib.ptr(oy, ctypes.c_int32),
+                _lib.ptr(rows, ctypes.c_int32), _lib.ptr(np.ascontiguousarray(zf), ctypes.c_double),
+                _lib.ptr(out, ctypes.c_int32)))
+            self.max_pc = (int(out[0]), int(out[1]), int(out[2]))
+            self._max_valid = True
+        return self.max_pc
+
+    step = update
+
+    def run(self, odometry):
+        """``update`` for every row (vtrans, vrot) of ``odometry``; one host round trip.
+
+        Returns an int32 array (n, 3) of max_pc per step.  A LUT KeyError at step
+        s leaves the state the reference would (steps < s done, then steps 1-4 of s).
+        """
+        od = np.asarray(odometry, dtype=np.float64).reshape(-1, 2)
+        n = od.shape[0]
+        ox, oy, rows, zf, first_bad = F.batch_control(od, self.shape[2], self.filter_table)
+        todo = n if first_bad is None else first_bad
+        out = np.empty((n, 3), dtype=np.int32)
+        with self._mutex:
+            if todo > 0:
+                _lib.check(self._lib.rs_pc_run(
+                    self._h, todo, _lib.ptr(ox, ctypes.c_int32), _lib.ptr(oy, ctypes.c_int32),
+                    _lib.ptr(rows, ctypes.c_int32), _lib.ptr(zf, ctypes.c_double),
+                    _lib.ptr(out, ctypes.c_int32)))
+                self.max_pc = tuple(int(v) for v in out[todo - 1])
+                self._max_valid = True
+            if first_bad is not None:
+                _lib.check(self._lib.rs_pc_excite(self._h))
+                self._max_valid = False
+        if first_bad is not None:
+            F.step_control(od[first_bad, 0], od[first_bad, 1], self.shape[2], self.filter_table)
+            raise KeyError('LUT miss at step %d' % first_bad)  # pragma: no cover
+        return out
+
+    def device_ms(self):
+        """Device time (HIP events) of the last update/run, in ms."""
+        ms = ctypes.c_double()
+        _lib.check(self._lib.rs_pc_last_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
+    def set_profiling(self, enable=True):
+        _lib.check(self._lib.rs_pc_set_profiling(self._h, int(bool(enable))))
+
+    def kernel_ms(self):
+        """(excite_ms, path_ms) summed over the steps of the last run (profiling on)."""
+        ms = np.zeros(2)
+        _lib.check(self._lib.rs_pc_kernel_ms(self._h, _lib.ptr(ms, ctypes.c_double)))
+        return float(ms[0]), float(ms[1])
+
+    # -- filter helpers of the reference class (host-side, NumPy) -----------------
+    def diff_gaussian_offset_2d(self, sigma_e, sigma_i, shape=(7, 7), origin=(0, 0)):
+        return F.filter_2d(origin, sigma_e, sigma_i, shape)
+
+    def diff_gaussian_offset_1d(self, sigma_e, sigma_i, size=7, origin=0):
+        return np.array(F.filter_1d(origin, sigma_e, sigma_i, size))
+
+    def build_diff_gaussian_set_2d(self, sigma_e, sigma_i, shape=(7, 7), precision=1):
+        if precision != 1 or (sigma_e, sigma_i, tuple(shape)) != (PC_E_SIGMA, PC_I_SIGMA, (7, 7)):
+            span = range(-5 * precision, 5 * precision)
+            return {(x, y): F.filter_2d((x // (precision * 10), y // (precision * 10)),
+                                        sigma_e, sigma_i, shape) for x in span for y in span}
+        return dict(self.filter_dict_2d)
+
+    def filters_from_origins_approx(self, origins, shape=(7, 7)):
+        """LUT lookup per layer (posecell_network.py:244-250); KeyError on a miss."""
+        origins = np.asarray(origins)
+        keys = np.trunc(origins[0] * self.filter_dict_2d_precision).astype(np.int64)
+        rows = self.filter_table.rows_for_keys(keys)
+        return np.ascontiguousarray(np.moveaxis(self.filter_table.filters[rows], 0, -1))

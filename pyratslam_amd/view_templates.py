@@ -1,0 +1,283 @@
+"""Drop-in ``ViewTemplate`` / ``ViewTemplates`` backed by libratslam_hip.
+
+API of ``/root/reference/ratslam/view_templates.py``: ``ViewTemplates(x_range,
+y_range, x_step, y_step, im_x, im_y, match_threshold)`` with ``.match(input,
+pc_x, pc_y, pc_th)`` -> ``ViewTemplate`` (``.get_index()``, ``.location()``,
+``.template``, ``.match(other)``) and the ``.templates`` list.
+
+The library lives on the GPU (``csrc/view_templates.hip``); each match scans it
+with the wrapped-uint8 row-shift score and applies the reference's strict
+threshold / first-argmin / append-on-miss rule.  ``match_batch`` runs many
+matches with the exact sequential semantics in one call.
+``ShardedViewTemplates`` spreads the library over ranks (one GPU each).
+
+Frames must be ``uint8`` (the ROS path, ``ros_simulate.py:100-101``); the
+subsampling mask is the reference's, with Python-2 integer division (:44-54).
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib
+
+MAX_OFFSET = 8  # view_templates.py:14
+
+
+def py2_mask(x_range, y_range, x_step, y_step, im_x, im_y):
+    """``ViewTemplates.__init__`` mask and template shape (view_templates.py:42-57)."""
+    pix = np.arange(im_x * im_y)
+    r, c = np.divmod(pix, im_x)
+    keep = (r > y_range[0]) & (r < y_range[1]) & (c > x_range[0]) & (c < x_range[1])
+    keep &= ((r - y_range[0]) % y_step != 0) & ((c - x_range[0]) % x_step != 0)
+    shape = ((x_range[1] - x_range[0]) // x_step, (y_range[1] - y_range[0]) // y_step)
+    return keep.reshape((im_x, im_y)), shape
+
+
+class ViewTemplate:
+    """One stored view (view_templates.py:4-37)."""
+
+    def __init__(self, pc_x, pc_y, pc_th, index, template, _owner=None):
+        self.pc_x = pc_x
+        self.pc_y = pc_y
+        self.pc_th = pc_th
+        self.template = template
+        self.index = index
+        self.max_offset = MAX_OFFSET
+        self._owner = _owner
+        self._solo = None
+
+    def match(self, new_template):
+        """Row-shift score against ``new_template`` (view_templates.py:16-28), on the GPU."""
+        q = np.ascontiguousarray(new_template)
+        if self._owner is not None and self._owner.nranks == 1:
+            return self._owner.scores(q[None], self.index, 1)[0, 0]
+        if self._solo is None:
+            t = np.ascontiguousarray(self.template)
+            self._solo = ViewTemplates._from_shape(t.shape, np.iinfo(np.uint64).max)
+            self._solo.add(t[None])
+        return self._solo.scores(q[None], 0, 1)[0, 0]
+
+    def location(self):
+        return (self.pc_x, self.pc_y, self.pc_th)
+
+    def get_index(self):
+        return self.index
+
+
+class ViewTemplates:
+    """Library of view templates on one GPU (view_templates.py:40-75)."""
+
+    def __init__(self, x_range, y_range, x_step, y_step, im_x, im_y, match_threshold,
+                 device=0, capacity=1024):
+        self.mask, self.shape = py2_mask(x_range, y_range, x_step, y_step, im_x, im_y)
+        self._init_device(self.shape, match_threshold, device, capacity)
+
+    @classmethod
+    def _from_shape(cls, shape, match_threshold, device=0, capacity=64):
+        self = cls.__new__(cls)
+        self.mask = None
+        self.shape = tuple(int(s) for s in shape)
+        self._init_device(self.shape, match_threshold, device, capacity)
+        return self
+
+    def _init_device(self, shape, match_threshold, device, capacity):
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.match_threshold = match_threshold
+        self.templates = []
+        self.device = int(device)
+        self.rank, self.nranks = 0, 1
+        self._mutex = threading.Lock()
+        self._h = None
+        self._lib = _lib.require_device()
+        # scores are integers, so `score > t` == `score > floor(t)` (view_templates.py:67)
+        if not match_threshold >= 0:
+            raise ValueError('match_threshold must be >= 0, got %r' % (match_threshold,))
+        thr = min(int(np.floor(match_threshold)), int(np.iinfo(np.uint64).max))
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.rs_vt_create(self.shape[0], self.shape[1], MAX_OFFSET, thr,
+                                          int(capacity), self.device, ctypes.byref(h)))
+        self._h = h
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            self._lib.rs_vt_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return len(self.templates)
+
+    def __getitem__(self, index):
+        return self.templates[index]
+
+    # -- helpers ----------------------------------------------------------------
+    def subsample(self, image):
+        """``input[self.mask].reshape(self.shape)`` (view_templates.py:64)."""
+        im = np.asarray(image)
+        if im.dtype != np.uint8:
+            raise TypeError('ViewTemplates matches uint8 frames (mono8, ros_simulate.py:100-101); '
+                            'got %s' % im.dtype)
+        if im.shape != self.mask.shape:
+            raise ValueError('frame shape %r does not match the mask %r' % (im.shape, self.mask.shape))
+        return im[self.mask].reshape(self.shape)
+
+    def _check_templates(self, t):
+        t = np.asarray(t)
+        if t.dtype != np.uint8:
+            raise TypeError('templates must be uint8, got %s' % t.dtype)
+        if t.shape[-2:] != self.shape:
+            raise ValueError('template shape %r != %r' % (t.shape[-2:], self.shape))
+        return np.ascontiguousarray(t.reshape((-1,) + self.shape))
+
+    def count(self):
+        c = ctypes.c_int64()
+        _lib.check(self._lib.rs_vt_count(self._h, ctypes.byref(c)))
+        return c.value
+
+    def add(self, templates, locations=None):
+        """Append templates unconditionally (indices len .. len+n-1)."""
+        t = self._check_templates(templates)
+        first = ctypes.c_int64()
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_add(self._h, t.shape[0], _lib.ptr(t, ctypes.c_uint8),
+                                           ctypes.byref(first)))
+            for i in range(t.shape[0]):
+                loc = locations[i] if locations is not None else (0, 0, 0)
+                self.templates.append(ViewTemplate(loc[0], loc[1], loc[2], first.value + i, t[i],
+                                                   _owner=self))
+        return first.value
+
+    def scores(self, queries, t0=0, nt=None):
+        """uint64 (nq, nt) scores of queries vs templates [t0, t0+nt) -- ViewTemplate.match."""
+        q = self._check_templates(queries)
+        nt = self.count() - t0 if nt is None else nt
+        out = np.empty((q.shape[0], nt), dtype=np.uint64)
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_scores(self._h, q.shape[0], _lib.ptr(q, ctypes.c_uint8),
+                                              int(t0), int(nt), _lib.ptr(out, ctypes.c_uint64)))
+        return out
+
+    # -- matching ----------------------------------------------------------------
+    def _record(self, q, pcs, idx, new):
+        for i in range(q.shape[0]):
+            if new[i]:
+                assert idx[i] == len(self.templates), (idx[i], len(self.templates))
+                p = pcs[i]
+                self.templates.append(ViewTemplate(p[0], p[1], p[2], int(idx[i]), q[i].copy(),
+                                                   _owner=self))
+        return [self.templates[int(j)] for j in idx]
+
+    def match_templates(self, queries, pcs=None, mode=_lib.RS_VT_SEQUENTIAL):
+        """Match already-subsampled (nq, H, W) queries; returns (index, score, is_new)."""
+        q = self._check_templates(queries)
+        n = q.shape[0]
+        idx = np.empty(n, dtype=np.int64)
+        score = np.empty(n, dtype=np.uint64)
+        new = np.zeros(n, dtype=np.uint8)
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_match_batch(
+                self._h, n, _lib.ptr(q, ctypes.c_uint8), mode, _lib.ptr(score, ctypes.c_uint64),
+                _lib.ptr(idx, ctypes.c_int64), _lib.ptr(new, ctypes.c_uint8)))
+            if mode == _lib.RS_VT_SEQUENTIAL:
+                self._record(q, pcs if pcs is not None else [(0, 0, 0)] * n, idx, new)
+        return idx, score, new.astype(bool)
+
+    def match(self, input, pc_x, pc_y, pc_th):
+        """Best template for a frame, or a new one (view_templates.py:63-75)."""
+        t = self.subsample(input)
+        idx, _, _ = self.match_templates(t[None], [(pc_x, pc_y, pc_th)])
+        return self.templates[int(idx[0])]
+
+    def match_batch(self, images, pcs):
+        """``[match(im, *pc) for im, pc in zip(images, pcs)]`` in one call."""
+        q = np.stack([self.subsample(im) for im in images])
+        idx, _, _ = self.match_templates(q, pcs)
+        return [self.templates[int(i)] for i in idx]
+
+    def device_ms(self):
+        ms = ctypes.c_double()
+        _lib.check(self._lib.rs_vt_last_ms(self._h, ctypes.byref(ms)))
+        return ms.value
+
+
+class ShardedViewTemplates(ViewTemplates):
+    """Template library sharded round-robin over ranks (template g on rank g % n).
+
+    ``reducer`` combines the per-rank first-argmin keys (uint64, key = score << 32
+    | g, UINT64_MAX = none):
+      * ``'rccl'``: an RCCL allreduce(min) on the GPU inside the library; every
+        rank calls ``rs_comm_unique_id`` on rank 0's id (``unique_id`` bytes);
+      * a callable ``f(keys: uint64 ndarray) -> uint64 ndarray`` returning the
+        elementwise min over ranks (e.g. torch.distributed all_reduce MIN).
+    Every rank sees all queries and keeps the full ``.templates`` metadata; the
+    template bytes of g live only on rank g % n.
+    """
+
+    def __init__(self, x_range, y_range, x_step, y_step, im_x, im_y, match_threshold,
+                 rank, nranks, reducer='rccl', unique_id=None, device=0, capacity=1024):
+        self.mask, self.shape = py2_mask(x_range, y_range, x_step, y_step, im_x, im_y)
+        self._init_device(self.shape, match_threshold, device, capacity)
+        self._attach(rank, nranks, reducer, unique_id)
+
+    @classmethod
+    def from_shape(cls, shape, match_threshold, rank, nranks, reducer='rccl', unique_id=None,
+                   device=0, capacity=1024):
+        self = cls.__new__(cls)
+        self.mask = None
+        self._init_device(shape, match_threshold, device, capacity)
+        self._attach(rank, nranks, reducer, unique_id)
+        return self
+
+    def _attach(self, rank, nranks, reducer, unique_id):
+        self.rank, self.nranks = int(rank), int(nranks)
+        self.reducer = reducer
+        if reducer == 'rccl':
+            if unique_id is None or len(unique_id) != _lib.RS_UNIQUE_ID_BYTES:
+                raise ValueError('reducer="rccl" needs the %d-byte unique id from rank 0'
+                                 % _lib.RS_UNIQUE_ID_BYTES)
+            uid = np.frombuffer(bytes(unique_id), dtype=np.uint8).copy()
+            _lib.check(self._lib.rs_vt_attach_comm(self._h, self.rank, self.nranks,
+                                                   _lib.ptr(uid, ctypes.c_uint8)))
+        elif callable(reducer):
+            _lib.check(self._lib.rs_vt_set_shard(self._h, self.rank, self.nranks))
+        else:
+            raise ValueError('reducer must be "rccl" or a callable')
+
+    @staticmethod
+    def unique_id():
+        """RCCL unique id (bytes) to broadcast from rank 0."""
+        lib = _lib.require_device()
+        buf = np.zeros(_lib.RS_UNIQUE_ID_BYTES, dtype=np.uint8)
+        _lib.check(lib.rs_comm_unique_id(_lib.ptr(buf, ctypes.c_uint8)))
+        return buf.tobytes()
+
+    def match_templates(self, queries, pcs=None, mode=_lib.RS_VT_SEQUENTIAL):
+        if self.reducer == 'rccl':
+            return super().match_templates(queries, pcs, mode)
+        q = self._check_templates(queries)
+        n = q.shape[0]
+        local = np.empty(n, dtype=np.uint64)
+        idx = np.empty(n, dtype=np.int64)
+        score = np.empty(n, dtype=np.uint64)
+        new = np.zeros(n, dtype=np.uint8)
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_scan_local(self._h, n, _lib.ptr(q, ctypes.c_uint8),
+                                                  _lib.ptr(local, ctypes.c_uint64)))
+            glob = np.ascontiguousarray(self.reducer(local), dtype=np.uint64)
+            _lib.check(self._lib.rs_vt_resolve(
+                self._h, n, _lib.ptr(glob, ctypes.c_uint64), mode, _lib.ptr(score, ctypes.c_uint64),
+                _lib.ptr(idx, ctypes.c_int64), _lib.ptr(new, ctypes.c_uint8)))
+            if mode == _lib.RS_VT_SEQUENTIAL:
+                self._record(q, pcs if pcs is not None else [(0, 0, 0)] * n, idx, new)
+        return idx, score, new.astype(bool)
+
+    def add(self, templates, locations=None):
+        # every rank calls add with the same templates; rank g % n keeps the bytes
+        return super().add(templates, locations)

@@ -1,0 +1,105 @@
+"""Host-side control plane of the drop-in (pyratslam_amd.filters, view mask):
+every value handed to the GPU must be bit-identical to the reference's."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import posecell as P
+from oracle import view_templates as V
+from pyratslam_amd import filters as F
+from pyratslam_amd.view_templates import py2_mask
+
+
+def test_kernel_3d_matches_reference_bits():
+    assert np.array_equal(F.kernel_3d(), load_golden('kernels')['kernel_3d'])
+
+
+def test_separable_factors_reconstruct_kernel():
+    ge, gi, scale = F.separable_factors()
+    k = (np.einsum('i,j,k->ijk', ge, ge, ge) - np.einsum('i,j,k->ijk', gi, gi, gi)) * scale
+    assert np.abs(k - load_golden('kernels')['kernel_3d']).max() < 2e-16 * 8
+
+
+def test_filter_table_matches_lut():
+    g = load_golden('kernels')
+    t = F.FilterTable()
+    assert t.filters.shape == (4, 7, 7)   # Py2: origins in {-1, 0}^2
+    for key, f in zip(g['lut_keys'], g['lut_filters']):
+        assert np.array_equal(t.dict[tuple(int(v) for v in key)], f)
+
+
+def test_filter_1d_bits_and_cache():
+    g = load_golden('kernels')
+    for o, f in zip(g['f1d_origins'], g['f1d']):
+        assert np.array_equal(F.filter_1d(int(o)), f)
+        assert F.filter_1d(int(o)) is F.filter_1d(int(o))
+
+
+def _odometry(n, seed):
+    r = np.random.default_rng(seed)
+    return np.stack([r.uniform(0, 0.6, n), r.uniform(-0.15, 0.15, n)], axis=1)
+
+
+@pytest.mark.parametrize('th', [10, 18, 36, 72])
+def test_step_control_matches_oracle(th):
+    table = F.FilterTable()
+    lut = P.lut_2d()
+    od = np.concatenate([_odometry(200, th), [[3.0, np.pi / 4], [3.0, 0.0], [0.0, 0.0]]])
+    for vt, vr in od:
+        try:
+            ref = P.step_control(vt, vr, (8, 8, th), lut)
+        except KeyError:
+            with pytest.raises(KeyError):
+                F.step_control(vt, vr, th, table)
+            continue
+        ox, oy, rows, zf, radius = F.step_control(vt, vr, th, table)
+        assert np.array_equal(ox, ref['ox']) and np.array_equal(oy, ref['oy'])
+        assert np.array_equal(zf, ref['zf'])
+        assert radius == ref['radius']
+        assert np.array_equal(table.filters[rows], np.moveaxis(ref['filters'], -1, 0))
+
+
+def test_batch_control_equals_step_control():
+    table = F.FilterTable()
+    od = _odometry(300, 7)
+    ox, oy, rows, zf, bad = F.batch_control(od, 36, table)
+    assert bad is None
+    for s in range(len(od)):
+        a = F.step_control(od[s, 0], od[s, 1], 36, table)
+        assert np.array_equal(ox[s], a[0]) and np.array_equal(oy[s], a[1])
+        assert np.array_equal(rows[s], a[2]) and np.array_equal(zf[s], a[3])
+
+
+def test_keyerror_at_half_cell():
+    # vtrans = 0.1 m = 0.5 cell: around(0.5) = 0 -> residual 0.5 -> key 5 (posecell_network.py:249)
+    table = F.FilterTable()
+    with pytest.raises(KeyError) as e:
+        F.step_control(0.1, 0.0, 18, table)
+    assert e.value.args[0] == (5, 5)
+    od = np.array([[0.2, 0.0], [0.3, 0.01], [0.1, 0.0], [0.2, 0.0]])
+    *_, bad = F.batch_control(od, 18, table)
+    assert bad == 2
+
+
+def test_simulate_scenario_half_boundaries():
+    # simulate.py: vtrans 3 m -> 15 cells; 15*cos(60 deg) sits on a .5 rounding edge
+    table = F.FilterTable()
+    lut = P.lut_2d()
+    for th in (10, 36):
+        ref = P.step_control(3.0, np.pi / 4, (8, 8, th), lut)
+        ox, oy, rows, zf, _ = F.step_control(3.0, np.pi / 4, th, table)
+        assert np.array_equal(ox, ref['ox']) and np.array_equal(oy, ref['oy'])
+        assert math.floor((np.pi / 4) / (2 * np.pi / th) + .5) == ref['z_origin']
+
+
+@pytest.mark.parametrize('name', ['vt_trace_ros', 'vt_trace_64x32'])
+def test_view_mask_matches_reference(name):
+    d = load_golden(name)
+    p = d['params']
+    mask, shape = py2_mask((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7])
+    assert np.array_equal(mask, d['mask'])
+    assert shape == tuple(d['shape'])
+    m2, s2 = V.py2_mask((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7])
+    assert np.array_equal(mask, m2) and shape == s2

@@ -1,0 +1,93 @@
+"""Pin the CPU oracle to the reference: every golden vector produced by running
+the reference itself (tests/golden/gen_golden.py) must be reproduced exactly."""
+import numpy as np
+import pytest
+
+from conftest import dense_state, load_golden
+from oracle import posecell as P
+from oracle import view_templates as V
+
+PC_CASES = ['pc32_s0', 'pc32_s1', 'pc32_s2', 'pc_ros21', 'pc_simulate', 'pc_ragged', 'pc64_s0']
+
+
+def test_kernel_3d_bit_exact():
+    k = load_golden('kernels')
+    assert np.array_equal(P.dog_kernel_3d(), k['kernel_3d'])
+    # posecell_network.py:97-113 known answer
+    assert k['kernel_3d'][3, 3, 3] == 0.2610825802870828
+
+
+def test_kernel_3d_is_rank2_separable():
+    ge, gi, s = P.gauss_1d_factors()
+    sep = (np.einsum('i,j,k->ijk', ge, ge, ge) - np.einsum('i,j,k->ijk', gi, gi, gi)) / s
+    assert np.abs(sep - load_golden('kernels')['kernel_3d']).max() < 1e-15
+
+
+def test_lut_py2_bit_exact():
+    k = load_golden('kernels')
+    lut = P.lut_2d()
+    assert len(lut) == len(k['lut_keys']) == 100
+    for key, f in zip(k['lut_keys'], k['lut_filters']):
+        assert np.array_equal(lut[tuple(int(v) for v in key)], f)
+
+
+def test_filter_1d_bit_exact():
+    k = load_golden('kernels')
+    for o, f in zip(k['f1d_origins'], k['f1d']):
+        assert np.array_equal(P.dog_offset_1d(int(o)), f)
+    assert np.array_equal(P.dog_offset_2d((0, 0)), k['f2d_origin0'])
+
+
+@pytest.mark.parametrize('name', PC_CASES)
+def test_posecell_trajectory_bit_exact(name):
+    case = load_golden(name)
+    net = P.PoseCellOracle(tuple(case['shape']))
+    net.inject(1, tuple(case['inject']))
+    steps = len(case['odom']) if name != 'pc64_s0' else 4
+    for s in range(steps):
+        m = net.update(case['odom'][s])
+        assert m == tuple(case['max_pc'][s])
+        assert np.array_equal(net.posecells, dense_state(case, s)), (name, s)
+
+
+def test_keyerror_parity():
+    case = load_golden('pc_keyerror')
+    assert str(case['raised']) == '(5, 5)'
+    net = P.PoseCellOracle(tuple(case['shape']))
+    net.inject(1, (16, 16, 9))
+    with pytest.raises(KeyError) as e:
+        net.update(case['odom'][0])
+    assert e.value.args[0] == (5, 5)
+
+
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_vt_pair_scores_bit_exact(i):
+    d = load_golden('vt_pairs')
+    a, b, s = d[f'u8_{i}_a'], d[f'u8_{i}_b'], d[f'u8_{i}_score']
+    for j in range(len(a)):
+        assert V.vt_score(a[j], b[j]) == s[j]
+        assert V.vt_scores_library(a[j:j + 1], b[j])[0] == s[j]
+        assert V.vt_score(a[j].astype(np.float64), b[j].astype(np.float64)) == d[f'f64_{i}_score'][j]
+
+
+def test_vt_wraps_uint8():
+    # wrapped sum 188,233 vs float SAD 124,981 for rng(1) pairs
+    rng = np.random.default_rng(1)
+    a = rng.integers(0, 256, (64, 32), dtype=np.uint8)
+    b = rng.integers(0, 256, (64, 32), dtype=np.uint8)
+    wrapped = V.vt_score(a, b)
+    sad = V.vt_score(a.astype(np.int64), b.astype(np.int64))
+    assert wrapped != sad and wrapped > sad
+
+
+@pytest.mark.parametrize('name', ['vt_trace_ros', 'vt_trace_64x32'])
+def test_vt_trace_bit_exact(name):
+    d = load_golden(name)
+    p = d['params']
+    o = V.ViewTemplatesOracle((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    assert np.array_equal(o.mask, d['mask'])
+    assert o.shape == tuple(d['shape'])
+    idx = [o.match_template(q, *pc)[0] for q, pc in zip(d['queries'], d['pcs'])]
+    assert np.array_equal(idx, d['index'])
+    assert np.array_equal(np.stack(o.templates), d['templates'])
+    assert np.array_equal(np.array(o.locations), d['locations'])

@@ -1,0 +1,167 @@
+"""Pose-cell network on the GPU vs the reference (golden trajectories) and the
+oracle.  Tolerance (BASELINE.json north_star): float32 activations within 1e-5
+of the float64 reference, argmax identical; float64 path within 1e-12."""
+import numpy as np
+import pytest
+
+from conftest import dense_state, load_golden
+from oracle import posecell as P
+
+pytestmark = pytest.mark.gpu
+
+F32_TOL = 1e-5
+F64_TOL = 1e-12
+CASES = ['pc32_s0', 'pc32_s1', 'pc32_s2', 'pc_ros21', 'pc_simulate', 'pc_ragged', 'pc64_s0']
+
+
+@pytest.fixture(scope='module')
+def pcn():
+    from pyratslam_amd import _build
+    _build.build()
+    from pyratslam_amd import PoseCellNetwork
+    return PoseCellNetwork
+
+
+def odometry(n, seed, vmax=0.6, rmax=0.15):
+    r = np.random.default_rng(seed)
+    return np.stack([r.uniform(0, vmax, n), r.uniform(-rmax, rmax, n)], axis=1)
+
+
+@pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
+@pytest.mark.parametrize('name', CASES)
+def test_golden_trajectory(pcn, name, precision, tol):
+    case = load_golden(name)
+    net = pcn(tuple(case['shape']), precision=precision)
+    net.inject(1, tuple(case['inject']))
+    worst = 0.0
+    for s, v in enumerate(case['odom']):
+        m = net.update(v)
+        assert m == tuple(case['max_pc'][s]), (name, s)
+        assert net.max_pc == m
+        worst = max(worst, np.abs(net.posecells - dense_state(case, s)).max())
+    assert worst < tol, worst
+
+
+def test_run_equals_repeated_update(pcn):
+    od = odometry(64, 11)
+    a = pcn((32, 32, 18))
+    b = pcn((32, 32, 18))
+    a.inject(1, (16, 16, 9))
+    b.inject(1, (16, 16, 9))
+    maxes = a.run(od)
+    for s, v in enumerate(od):
+        assert b.update(v) == tuple(maxes[s])
+    assert np.array_equal(a.posecells, b.posecells)   # same kernels, deterministic
+
+
+@pytest.mark.parametrize('shape,steps', [((64, 64, 36), 30), ((48, 40, 20), 30)])
+def test_random_odometry_vs_oracle(pcn, shape, steps):
+    od = odometry(steps, 5)
+    net = pcn(shape)
+    ref = P.PoseCellOracle(shape)
+    loc = tuple(s // 2 for s in shape)
+    net.inject(1, loc)
+    ref.inject(1, loc)
+    got = net.run(od)
+    for s in range(steps):
+        assert tuple(got[s]) == ref.update(od[s])
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+
+
+def test_large_grid_properties(pcn):
+    """128x128x72 (BASELINE config 4): parity on two steps vs the oracle, then
+    size-independent properties over a long rollout: non-negative, finite,
+    float32 == float64 device paths within tolerance, argmax agreement."""
+    shape = (128, 128, 72)
+    od = odometry(40, 9)
+    a, b = pcn(shape), pcn(shape, precision='float64')
+    ref = P.PoseCellOracle(shape)
+    for n in (a, b, ref):
+        n.inject(1, (64, 64, 36))
+    for s in range(2):
+        m = ref.update(od[s])
+        assert a.update(od[s]) == m and b.update(od[s]) == m
+    assert np.abs(a.posecells - ref.posecells).max() < F32_TOL
+    assert np.abs(b.posecells - ref.posecells).max() < F64_TOL
+    ma, mb = a.run(od[2:]), b.run(od[2:])
+    assert np.array_equal(ma, mb)
+    pa, pb = a.posecells, b.posecells
+    assert np.isfinite(pa).all() and (pa >= 0).all()
+    assert np.abs(pa - pb).max() < F32_TOL
+
+
+def test_keyerror_leaves_reference_state(pcn):
+    case = load_golden('pc_keyerror')
+    shape = tuple(case['shape'])
+    net = pcn(shape, precision='float64')
+    net.inject(1, (16, 16, 9))
+    with pytest.raises(KeyError) as e:
+        net.update(case['odom'][0])
+    assert e.value.args[0] == (5, 5)
+    ref = P.PoseCellOracle(shape)
+    ref.inject(1, (16, 16, 9))
+    ref.excite_inhibit_normalise()
+    assert np.abs(net.posecells - ref.posecells).max() < F64_TOL
+    # batched: steps before the bad one run, then steps 1-4 of it, then KeyError
+    net2 = pcn(shape, precision='float64')
+    net2.inject(1, (16, 16, 9))
+    with pytest.raises(KeyError):
+        net2.run([[0.2, 0.0], [0.1, 0.0]])
+    ref2 = P.PoseCellOracle(shape)
+    ref2.inject(1, (16, 16, 9))
+    ref2.update((0.2, 0.0))
+    ref2.excite_inhibit_normalise()
+    assert np.abs(net2.posecells - ref2.posecells).max() < F64_TOL
+
+
+def test_state_roundtrip_inject_and_argmax(pcn):
+    rng = np.random.default_rng(3)
+    shape = (21, 21, 36)
+    for precision in ('float32', 'float64'):
+        net = pcn(shape, precision=precision)
+        assert (net.posecells == 0).all()
+        assert net.get_pc_max() == (0, 0, 0)          # argmax of zeros = first cell
+        v = rng.random(shape)
+        net.posecells = v
+        back = net.posecells
+        if precision == 'float64':
+            assert np.array_equal(back, v)
+        else:
+            assert np.array_equal(back, v.astype(np.float32).astype(np.float64))
+        assert net.get_pc_max() == tuple(np.unravel_index(np.argmax(back), shape))
+        net.inject(5.0, (3, 4, 5))
+        assert net.get_pc_max() == (3, 4, 5)
+        assert abs(net.total() - back.sum() - 5.0) < 1e-6 * back.size
+        net.inject(1.0, (-1, -1, -1))                 # numpy negative indexing
+        assert net.posecells[-1, -1, -1] == pytest.approx(back[-1, -1, -1] + 1.0, rel=1e-6)
+
+
+def test_argmax_first_maximum_tie_break(pcn):
+    shape = (8, 8, 8)
+    net = pcn(shape, precision='float64')
+    v = np.zeros(shape)
+    v[5, 1, 2] = v[2, 7, 7] = v[2, 7, 1] = 1.0
+    net.posecells = v
+    assert net.get_pc_max() == (2, 7, 1)
+
+
+def test_bad_inputs_raise(pcn):
+    with pytest.raises(ValueError):
+        pcn((2, 8, 8))
+    net = pcn((8, 8, 8))
+    with pytest.raises(TypeError):
+        net.posecells = np.zeros((8, 8, 7))
+    with pytest.raises(TypeError):
+        net.inject(1, [1, 2, 3])
+    with pytest.raises(IndexError):
+        net.inject(1, (8, 0, 0))
+
+
+def test_simulate_driver(pcn):
+    """simulate.py:36-41 scenario through the headless driver."""
+    from pyratslam_amd.simulate import RatSLAM, scenario
+    case = load_golden('pc_simulate')
+    sim = RatSLAM(data=scenario(), shape=(50, 50, 10))
+    for s in range(40):
+        sim.step()
+        assert sim.current_pose_cell == tuple(case['max_pc'][s])

@@ -1,0 +1,205 @@
+"""View-template matcher on the GPU: bit-exact scores and template indices vs the
+reference's golden vectors and the oracle (integer work -> exact equality)."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import view_templates as V
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def vtmod():
+    from pyratslam_amd import _build
+    _build.build()
+    import pyratslam_amd.view_templates as m
+    return m
+
+
+def image_from_template(mask, template):
+    im = np.zeros(mask.shape, dtype=np.uint8)
+    im[mask] = template.ravel()
+    return im
+
+
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_pair_scores_bit_exact(vtmod, i):
+    d = load_golden('vt_pairs')
+    a, b, s = d[f'u8_{i}_a'], d[f'u8_{i}_b'], d[f'u8_{i}_score']
+    lib = vtmod.ViewTemplates._from_shape(a.shape[1:], 45000)
+    lib.add(a)
+    sc = lib.scores(b)                        # (query, template)
+    assert np.array_equal(np.diagonal(sc), s)
+    # ViewTemplate.match on owned templates
+    assert lib.templates[3].match(b[3]) == s[3]
+
+
+@pytest.mark.parametrize('name', ['vt_trace_ros', 'vt_trace_64x32'])
+def test_trace_via_match(vtmod, name):
+    d = load_golden(name)
+    p = [int(v) for v in d['params']]
+    vts = vtmod.ViewTemplates((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    assert np.array_equal(vts.mask, d['mask'])
+    for q, pc, idx, cnt in zip(d['queries'], d['pcs'], d['index'], d['count']):
+        t = vts.match(image_from_template(vts.mask, q), *pc)
+        assert t.get_index() == idx
+        assert len(vts.templates) == cnt
+    assert np.array_equal(np.stack([t.template for t in vts.templates]), d['templates'])
+    assert np.array_equal(np.array([t.location() for t in vts.templates]), d['locations'])
+
+
+@pytest.mark.parametrize('name', ['vt_trace_ros', 'vt_trace_64x32'])
+def test_trace_via_match_batch(vtmod, name):
+    d = load_golden(name)
+    p = [int(v) for v in d['params']]
+    vts = vtmod.ViewTemplates((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    half = len(d['queries']) // 2
+    idx1, _, _ = vts.match_templates(d['queries'][:half], d['pcs'][:half])
+    idx2, _, _ = vts.match_templates(d['queries'][half:], d['pcs'][half:])
+    assert np.array_equal(np.concatenate([idx1, idx2]), d['index'])
+    assert np.array_equal(np.stack([t.template for t in vts.templates]), d['templates'])
+    for i in (0, len(vts.templates) - 1):
+        assert vts.templates[i].location() == tuple(d['locations'][i])
+
+
+@pytest.mark.parametrize('t,q,h,w', [(1000, 256, 64, 32), (130, 40, 32, 32), (3000, 7, 64, 32),
+                                     (200, 33, 24, 20), (70, 9, 17, 5)])
+def test_frozen_scan_vs_oracle(vtmod, t, q, h, w):
+    lib_np = V.synthetic_library(t, h, w, seed=t)
+    queries, src = V.synthetic_queries(lib_np, q, seed=q)
+    lib = vtmod.ViewTemplates._from_shape((h, w), 45000)
+    lib.add(lib_np)
+    idx, score, new = lib.match_templates(queries, mode=0)
+    assert not new.any()
+    for i in range(q):
+        ref = V.vt_scores_library(lib_np, queries[i])
+        assert score[i] == ref.min(), i
+        assert idx[i] == int(np.argmin(ref)), i
+    assert len(lib.templates) == t
+
+
+def test_all_pair_scores_vs_oracle(vtmod):
+    lib_np = V.synthetic_library(150, 64, 32, seed=4)
+    queries, _ = V.synthetic_queries(lib_np, 20, seed=5)
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    lib.add(lib_np)
+    sc = lib.scores(queries)
+    ref = np.stack([V.vt_scores_library(lib_np, q) for q in queries])
+    assert np.array_equal(sc, ref)
+
+
+def test_sequential_batch_equals_oracle_sequence(vtmod):
+    """Exact ViewTemplates.match semantics inside one batch: later queries may hit
+    templates appended earlier in the same batch, first argmin wins."""
+    base = V.synthetic_library(40, 64, 32, seed=8)
+    rng = np.random.default_rng(9)
+    qs = []
+    for i in range(300):
+        b = base[int(rng.integers(0, 40))]
+        n = rng.integers(0, 3 if rng.random() < 0.8 else 60, b.shape)
+        qs.append(np.clip(np.roll(b, int(rng.integers(-6, 7)), axis=0).astype(int) - n, 0, 255))
+    qs = np.array(qs, dtype=np.uint8)
+    ref = V.ViewTemplatesOracle((0, 128), (0, 64), 2, 2, 8, 8, 45000)
+    ref.shape = (64, 32)
+    expect = [ref.match_template(q)[0] for q in qs]
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    got = np.concatenate([lib.match_templates(qs[i:i + 64])[0] for i in range(0, 300, 64)])
+    assert np.array_equal(got, expect)
+    assert np.array_equal(np.stack([t.template for t in lib.templates]), np.stack(ref.templates))
+
+
+def test_ties_pick_first_index(vtmod):
+    t = V.synthetic_library(5, 64, 32, seed=2)
+    lib_np = np.concatenate([t, t, t])                       # indices 0..4 repeated
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 10 ** 9)
+    lib.add(lib_np)
+    idx, score, _ = lib.match_templates(t, mode=0)
+    assert np.array_equal(idx, np.arange(5)) and (score == 0).all()
+
+
+def test_empty_library_appends(vtmod):
+    lib = vtmod.ViewTemplates._from_shape((32, 32), 0)
+    q = V.synthetic_library(3, 32, 32, seed=1)
+    idx, score, new = lib.match_templates(q)
+    assert list(idx) == [0, 1, 2] and new.all()
+    assert score[0] == np.iinfo(np.uint64).max           # nothing to compare against
+    idx, _, new = lib.match_templates(q)                   # exact copies: score 0 > 0 is False
+    assert list(idx) == [0, 1, 2] and not new.any()
+
+
+@pytest.mark.parametrize('nranks', [2, 3, 4])
+def test_sharded_ranks_simulated_on_one_gpu(vtmod, nranks):
+    """nranks handles on one GPU, each owning templates g % nranks == rank; the
+    elementwise min over their local keys plays the RCCL allreduce(min)."""
+    base = V.synthetic_library(60, 64, 32, seed=21)
+    queries, _ = V.synthetic_queries(base, 200, seed=22, hit_frac=0.7)
+    import ctypes
+    from pyratslam_amd import _lib
+    shards = [vtmod.ShardedViewTemplates.from_shape((64, 32), 45000, r, nranks, reducer=lambda k: k)
+              for r in range(nranks)]
+    pending = {}
+    single = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    for s in shards:
+        s.add(base[:30])
+    single.add(base[:30])
+    for lo in range(0, 200, 50):
+        batch = queries[lo:lo + 50]
+        # scan on every rank first (collective order), then resolve everywhere
+        for r, s in enumerate(shards):
+            local = np.empty(len(batch), dtype=np.uint64)
+            _lib.check(s._lib.rs_vt_scan_local(s._h, len(batch), _lib.ptr(batch, ctypes.c_uint8),
+                                               _lib.ptr(local, ctypes.c_uint64)))
+            pending[r] = local
+        glob = np.minimum.reduce([pending[r] for r in range(nranks)])
+        results = []
+        for s in shards:
+            idx = np.empty(len(batch), dtype=np.int64)
+            new = np.empty(len(batch), dtype=np.uint8)
+            _lib.check(s._lib.rs_vt_resolve(s._h, len(batch), _lib.ptr(glob, ctypes.c_uint64), 1,
+                                            None, _lib.ptr(idx, ctypes.c_int64),
+                                            _lib.ptr(new, ctypes.c_uint8)))
+            results.append(idx)
+        ref_idx, _, _ = single.match_templates(batch)
+        for idx in results:
+            assert np.array_equal(idx, ref_idx)
+    total = single.count()
+    assert all(s.count() == total for s in shards)
+    # every template readable on exactly its owner
+    for g in range(total):
+        s = shards[g % nranks]
+        out = np.empty((64, 32), dtype=np.uint8)
+        _lib.check(s._lib.rs_vt_read(s._h, g, _lib.ptr(out, ctypes.c_uint8)))
+        ref = np.empty((64, 32), dtype=np.uint8)
+        _lib.check(single._lib.rs_vt_read(single._h, g, _lib.ptr(ref, ctypes.c_uint8)))
+        assert np.array_equal(out, ref)
+
+
+def test_sharded_python_reducer_path(vtmod):
+    """ShardedViewTemplates with a callable reducer, one rank (reduce = identity)."""
+    base = V.synthetic_library(30, 64, 32, seed=31)
+    queries, _ = V.synthetic_queries(base, 64, seed=32)
+    s = vtmod.ShardedViewTemplates.from_shape((64, 32), 45000, 0, 1, reducer=lambda k: k)
+    s.add(base)
+    single = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    single.add(base)
+    assert np.array_equal(s.match_templates(queries)[0], single.match_templates(queries)[0])
+
+
+def test_type_and_shape_errors(vtmod):
+    vts = vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, 45000)
+    with pytest.raises(TypeError):
+        vts.match(np.zeros((256, 256), dtype=np.float32), 0, 0, 0)
+    with pytest.raises(ValueError):
+        vts.match(np.zeros((128, 128), dtype=np.uint8), 0, 0, 0)
+    with pytest.raises(ValueError):
+        vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, -1)
+
+
+def test_library_growth(vtmod):
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000, capacity=64)
+    data = V.synthetic_library(700, 64, 32, seed=41)
+    for lo in range(0, 700, 100):
+        lib.add(data[lo:lo + 100])
+    idx, score, _ = lib.match_templates(data[::37], mode=0)
+    assert np.array_equal(idx, np.arange(0, 700, 37)) and (score == 0).all()
