@@ -1,0 +1,340 @@
+#!/usr/bin/env python3
+"""Benchmark of the pyratslam hot path on MI355X (BASELINE.json metric).
+
+One JSON line on rank 0:
+  value        template compares/s of the whole job (all ranks): each step
+               matches a batch of `--queries` subsampled 64x32 uint8 views,
+               resident in HBM, against the whole library (`--templates-per-gpu`
+               per rank, sharded round-robin, first-argmin combined by one RCCL
+               allreduce(min, uint64) per batch).  Weak scaling: the library
+               grows with the number of GPUs.
+  pose_cell    64x64x36 pose-cell network steps/s (the other half of the
+               metric): batched `run()` (per-step control uploaded with the
+               odometry) and the per-call `update()` drop-in rate; replicated
+               per GPU (one network, nothing to shard).
+  roofline     dominant kernel = the template scan: SURVEY.md section 8(d)'s
+               2,048 algorithmic bytes per compare x compares per launch / the
+               scan kernel's average HIP-event duration; the pose-cell kernels'
+               roofline is in pose_cell.roofline (24 bytes per cell per step).
+  cpu_baseline the oracle (NumPy restatement of the reference) on this host's
+               cores, bounded sample, rank 0 at N=1.
+
+Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under
+torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+BYTES_PER_COMPARE = 64 * 32  # one stored 64x32 u8 template
+METRIC = 'pose-cell steps/sec (64×64×36) + template-compares/sec at 1/2/4/8 GPU'
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20, help='timed template batches')
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--queries', type=int, default=1024)
+    ap.add_argument('--templates-per-gpu', type=int, default=1000)
+    ap.add_argument('--pc-shape', default='64,64,36')
+    ap.add_argument('--pc-steps', type=int, default=2000, help='timed pose-cell steps')
+    ap.add_argument('--pc-warmup', type=int, default=200)
+    ap.add_argument('--pc-calls', type=int, default=1000, help='timed per-call update()s')
+    ap.add_argument('--cpu-seconds', type=float, default=8.0, help='CPU baseline budget per leg')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
+    return ap.parse_args()
+
+
+class Dist:
+    """Control plane: gloo process group for the barrier, the RCCL unique-id
+    broadcast and the max-over-ranks time.  N = 1 needs no torch at all."""
+
+    def __init__(self, gpus):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        if self.world != gpus:
+            raise SystemExit('--gpus %d but WORLD_SIZE=%d: launch N>1 with '
+                             'python -m torch.distributed.run --nproc-per-node N bench.py --gpus N'
+                             % (gpus, self.world))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b):
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def min_keys(self, keys):
+        import torch
+        k = torch.from_numpy(keys.astype(np.uint64).view(np.int64).copy())
+        k[k == -1] = np.iinfo(np.int64).max          # UINT64_MAX (no template) -> int64 max
+        self.dist.all_reduce(k, op=self.dist.ReduceOp.MIN)
+        out = k.numpy().copy()
+        out[out == np.iinfo(np.int64).max] = -1
+        return out.view(np.uint64)
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def bench_templates(args, d):
+    from pyratslam_amd import _lib, synthetic
+    from pyratslam_amd.view_templates import ShardedViewTemplates, ViewTemplates
+    T, Q, n = args.templates_per_gpu, args.queries, d.world
+    reduce_kind = 'none'
+    if n == 1:
+        vts = ViewTemplates._from_shape((64, 32), 45000, device=d.local, capacity=T)
+    else:
+        uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
+        try:
+            vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer='rccl',
+                                                  unique_id=uid, device=d.local, capacity=T)
+            reduce_kind = 'rccl-allreduce-min-u64'
+        except Exception as e:  # pragma: no cover - recorded, not hidden
+            print('rank %d: RCCL attach failed (%s); host gloo reduction' % (d.rank, e),
+                  file=sys.stderr)
+            vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
+                                                  device=d.local, capacity=T)
+            reduce_kind = 'gloo-host-min'
+    # every rank adds the whole global library; rank r keeps templates g % n == r
+    total = T * n
+    for lo in range(0, total, 8192):
+        vts.add(synthetic.library(min(8192, total - lo), seed=1, first=lo))
+    qlib = synthetic.library(min(total, 4096), seed=1)
+    queries, src = synthetic.queries(qlib, Q, seed=2)
+    lib = vts._lib
+    import ctypes
+    idx = np.empty(Q, dtype=np.int64)
+    score = np.empty(Q, dtype=np.uint64)
+    new = np.empty(Q, dtype=np.uint8)
+
+    def match(staged):
+        qp = None if staged else _lib.ptr(queries, ctypes.c_uint8)
+        if vts.nranks > 1 and vts.reducer != 'rccl':
+            local = np.empty(Q, dtype=np.uint64)
+            _lib.check(lib.rs_vt_scan_local(vts._h, Q, qp, _lib.ptr(local, ctypes.c_uint64)))
+            glob = np.ascontiguousarray(vts.reducer(local))
+            _lib.check(lib.rs_vt_resolve(vts._h, Q, _lib.ptr(glob, ctypes.c_uint64), 0,
+                                         _lib.ptr(score, ctypes.c_uint64),
+                                         _lib.ptr(idx, ctypes.c_int64), _lib.ptr(new, ctypes.c_uint8)))
+        else:
+            _lib.check(lib.rs_vt_match_batch(vts._h, Q, qp, _lib.RS_VT_FROZEN,
+                                             _lib.ptr(score, ctypes.c_uint64),
+                                             _lib.ptr(idx, ctypes.c_int64),
+                                             _lib.ptr(new, ctypes.c_uint8)))
+
+    match(staged=False)                      # stage the batch in HBM (+ correctness probe)
+    hits = src >= 0
+    correct = bool(np.all(idx[hits] == src[hits]))
+    for _ in range(args.warmup):
+        match(staged=True)
+    kernel_ms = []
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        match(staged=True)
+        kernel_ms.append(vts.device_ms())
+    t1 = time.perf_counter()
+    d.barrier()
+    dt = d.max(t1 - t0)
+    # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
+    d.barrier()
+    p0 = time.perf_counter()
+    for _ in range(max(3, args.steps // 4)):
+        match(staged=False)
+    p1 = time.perf_counter()
+    d.barrier()
+    dtp = d.max(p1 - p0)
+    compares = float(total) * Q
+    scan_ms = float(np.mean(kernel_ms))
+    res = {
+        'value': compares * args.steps / dt,
+        'ms_per_step': 1e3 * dt / args.steps,
+        'pcie_inclusive_value': compares * max(3, args.steps // 4) / dtp,
+        'scan_ms': scan_ms,
+        'compares_per_launch': float(T) * Q,
+        'reduce': reduce_kind,
+        'hits_correct': correct,
+        'templates_total': total,
+    }
+    vts.close()
+    return res
+
+
+def bench_posecells(args, d):
+    from pyratslam_amd import PoseCellNetwork, synthetic
+    shape = tuple(int(s) for s in args.pc_shape.split(','))
+    net = PoseCellNetwork(shape, device=d.local)
+    net.inject(1, tuple(s // 2 for s in shape))
+    od = synthetic.odometry(args.pc_warmup + args.pc_steps + args.pc_calls + 64, seed=0)
+    net.run(od[:args.pc_warmup])
+    d.barrier()
+    t0 = time.perf_counter()
+    net.run(od[args.pc_warmup:args.pc_warmup + args.pc_steps])
+    t1 = time.perf_counter()
+    d.barrier()
+    dt = d.max(t1 - t0)
+    # per-call drop-in rate: PoseCellNetwork.update() through ctypes, one sync each
+    base = args.pc_warmup + args.pc_steps
+    for v in od[base:base + 16]:
+        net.update(v)
+    c0 = time.perf_counter()
+    for v in od[base + 16:base + 16 + args.pc_calls]:
+        net.update(v)
+    c1 = time.perf_counter()
+    # kernel durations (HIP events around every launch) on a separate profiled run
+    nprof = min(args.pc_steps, 500)
+    net.set_profiling(True)
+    net.run(od[:nprof])
+    ex_ms, pi_ms = net.kernel_ms()
+    net.set_profiling(False)
+    per_step_kernel_ms = (ex_ms + pi_ms) / nprof
+    ncell = shape[0] * shape[1] * shape[2]
+    alg = 24.0 * ncell            # 3 stencil passes x (read + write) x 4 B
+    finite = bool(np.isfinite(net.posecells).all())
+    net.close()
+    return {
+        'shape': list(shape),
+        'steps_per_s': args.pc_steps / dt,
+        'update_calls_per_s': args.pc_calls / (c1 - c0),
+        'us_per_step': 1e6 * dt / args.pc_steps,
+        'kernel_us_per_step': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
+        'replicas': d.world,
+        'finite': finite,
+        'roofline': {'bound': 'hbm', 'achieved': alg / (per_step_kernel_ms * 1e-3) / 1e9,
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': alg / (per_step_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     'traffic': None,
+                     'note': '24 B/cell/step algorithmic over the two kernels\' summed '
+                             'HIP-event time; the 576 KiB volume is L2-resident and the '
+                             'step is launch/latency-bound at this size'},
+    }
+
+
+def cpu_baseline(args):
+    """Oracle (NumPy restatement of the reference) on this host, bounded sample."""
+    from oracle import posecell as P
+    from oracle import view_templates as V
+    from pyratslam_amd import synthetic
+    T = args.templates_per_gpu
+    lib = synthetic.library(T, seed=1)
+    qs, _ = synthetic.queries(lib, 256, seed=2)
+    n = 0
+    t0 = time.perf_counter()
+    while n < len(qs) and time.perf_counter() - t0 < args.cpu_seconds:
+        V.vt_scores_library(lib, qs[n])
+        n += 1
+    dt = time.perf_counter() - t0
+    vt = {'value': T * n / dt, 'unit': 'compares/s', 'cores': 1, 'kind': 'port',
+          'sample': '%d queries x %d stored 64x32 u8 templates, oracle/view_templates.py '
+                    '(NumPy, single thread)' % (n, T)}
+    shape = tuple(int(s) for s in args.pc_shape.split(','))
+    net = P.PoseCellOracle(shape)
+    net.inject(1, tuple(s // 2 for s in shape))
+    od = synthetic.odometry(1000, seed=0)
+    k = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        net.update(od[k])
+        k += 1
+    dt = time.perf_counter() - t0
+    pc = {'value': k / dt, 'unit': 'steps/s', 'cores': 1, 'kind': 'port',
+          'sample': '%d updates of a %s grid, oracle/posecell.py (NumPy float64, 343-tap '
+                    'direct correlation like the reference kernel, single thread)' % (k, shape)}
+    return vt, pc
+
+
+def main():
+    args = parse()
+    d = Dist(args.gpus)
+    tv = bench_templates(args, d)
+    pc = bench_posecells(args, d)
+    if d.rank != 0:
+        d.close()
+        return
+    roof = {
+        'bound': 'hbm',
+        'achieved': BYTES_PER_COMPARE * tv['compares_per_launch'] / (tv['scan_ms'] * 1e-3) / 1e9,
+        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'traffic': None,
+    }
+    roof['frac'] = roof['achieved'] / roof['peak']
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get('templates_per_gpu') == args.templates_per_gpu and tj.get('queries') == args.queries:
+                roof['traffic'] = tj.get('hbm_bytes_per_launch')
+                roof['traffic_source'] = os.path.relpath(args.traffic_json, ROOT)
+        except Exception:
+            pass
+    out = {
+        'metric': METRIC,
+        'value': tv['value'],
+        'unit': 'compares/s',
+        'n_gpus': d.world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': tv['ms_per_step'],
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'u8',
+        'data': 'synthetic (SURVEY.md 8(d): uniform u8 library, shifted+noised queries, '
+                'U(0,0.6) m / U(-0.15,0.15) rad odometry)',
+        'config': {
+            'workload': 'configs[1]: 64x64x36 pose-cell grid + %d stored 64x32 u8 templates per '
+                        'GPU, %d-query batches resident in HBM' % (args.templates_per_gpu, args.queries),
+            'templates_per_gpu': args.templates_per_gpu,
+            'templates_total': tv['templates_total'],
+            'queries_per_step': args.queries,
+            'template_shape': [64, 32],
+            'pose_cell_grid': pc['shape'],
+            'parallelism': 'library sharded over %d GPU(s), %s; pose cells replicated'
+                           % (d.world, tv['reduce']),
+        },
+        'roofline': roof,
+        'pose_cell': pc,
+        'template_scan': {'kernel_ms_per_launch': tv['scan_ms'],
+                          'pcie_inclusive_compares_per_s': tv['pcie_inclusive_value'],
+                          'known_answer_hits_correct': tv['hits_correct']},
+    }
+    if d.world == 1 and not args.no_cpu_baseline:
+        vt_cpu, pc_cpu = cpu_baseline(args)
+        out['cpu_baseline'] = vt_cpu
+        out['pose_cell']['cpu_baseline'] = pc_cpu
+    print(json.dumps(out), flush=True)
+    d.close()
+
+
+if __name__ == '__main__':
+    main()

@@ -137,7 +137,9 @@ int rs_vt_read(rs_vt* h, int64_t index, uint8_t* out);
 #define RS_VT_FROZEN     0   /* score against the current library only, never append   */
 #define RS_VT_SEQUENTIAL 1   /* exactly nq successive ViewTemplates.match calls          */
 
-/* Match nq queries (each H x W uint8, already subsampled).
+/* Match nq queries (each H x W uint8, already subsampled).  queries == NULL
+ * re-matches the batch staged on the device by the previous call (same nq):
+ * the queries stay resident in HBM across calls.
  * best_score[i]: the minimum score (UINT64_MAX if the library was empty)
  * best_index[i]: the index ViewTemplates.match returns (first argmin, or the
  *                new template's index when is_new[i] = 1)

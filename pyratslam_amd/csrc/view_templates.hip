@@ -486,9 +486,14 @@ int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries) {
     RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
     RS_CHECK(nq >= 0, RS_ERR_ARG, "negative query count");
     if (nq == 0) return RS_OK;
-    RS_CHECK(queries, RS_ERR_ARG, "null queries");
     RS_HIP(hipSetDevice(h->device));
-    RS_TRY(vt_stage_queries(h, nq, queries));
+    if (queries) {
+        RS_TRY(vt_stage_queries(h, nq, queries));
+    } else {
+        // re-match the queries already resident on the device (last staged batch)
+        RS_CHECK(nq == h->stagedQ, RS_ERR_STATE, "no staged batch of %d queries (have %d)", nq,
+                 h->stagedQ);
+    }
     RS_HIP(hipMemsetAsync(h->dBest, 0xFF, sizeof(unsigned long long) * nq, h->stream));
     const int64_t lc = local_count_of(h, h->count);
     ScanOut out{h->dBest, nullptr, 0};
@@ -671,6 +676,7 @@ int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
     const size_t qb = (size_t)h->H * h->W * n;
     std::memcpy(h->hQraw, templates, qb);
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    h->stagedQ = 0;  // the staging buffer now holds templates, not a query batch
     std::vector<std::pair<int, int64_t>> news;
     news.reserve(n);
     for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
@@ -767,6 +773,7 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
     RS_CHECK(queries && scores, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(vt_stage_queries(h, nq, queries));
+    h->stagedQ = nq;
     const int64_t ld = (int64_t)rs::round_up((size_t)h->count, 64);
     RS_TRY(vt_grow_matrix(h, (size_t)ld * nq));
     ScanOut mo{nullptr, h->dMat, ld};
