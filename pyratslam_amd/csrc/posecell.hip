@@ -299,6 +299,292 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// Row-tiled forms (the fast path for Y <= 128).  A block owns BK layers x BX
+// rows x the whole Y extent; lanes own columns, so the periodic wrap in y is a
+// 3-cell LDS halo copy and no hot loop divides.  Every load a wave needs is
+// issued before the first LDS store (registers), the 7-tap y and x passes of
+// the excitation and the 7x7 path-integration stencil are register-blocked
+// per column (a lane walks the x direction of its column).
+// ---------------------------------------------------------------------------
+constexpr int RT_BX = 4, RT_BK = 2;
+
+// v in [-k*n, (k+1)*n) for small k (halo coordinates) -> [0, n)
+__device__ inline int wrap_small(int v, int n) {
+    while (v < 0) v += n;
+    while (v >= n) v -= n;
+    return v;
+}
+
+template <typename T, int YP>
+__global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T* __restrict__ Q,
+                                                      double* __restrict__ part,
+                                                      unsigned long long* __restrict__ res_slot,
+                                                      int X, int Y, int TH, SepKernel<T> k) {
+    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF;
+    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = (NR + 3) / 4;
+    __shared__ T s_in[NR * RW];
+    __shared__ T s_e[HK * BX * YP];
+    __shared__ T s_i[HK * BX * YP];
+    __shared__ double s_red[NT / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
+    if (res_slot != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0)
+        *res_slot = 0ull;  // the path kernel of this step max-reduces into it
+
+    T v[RPW][JC];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int row = wave + 4 * q;
+        const int kk = row / HX, a = row - kk * HX;
+        const int L = wrap_small(k0 - HALF + kk, TH), r = wrap_small(i0 - HALF + a, X);
+        const T* src = P + ((size_t)L * X + r) * Y;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int c = lane + 64 * jc;
+            v[q][jc] = (row < NR && c < Y) ? src[c] : T(0);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int row = wave + 4 * q;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int c = lane + 64 * jc;
+            if (row < NR && c < Y) {
+                T* dst = s_in + row * RW;
+                dst[HALF + c] = v[q][jc];
+                if (c < HALF) dst[HALF + Y + c] = v[q][jc];
+                if (c >= Y - HALF) dst[c - (Y - HALF)] = v[q][jc];
+            }
+        }
+    }
+    __syncthreads();
+
+    // y pass (7 taps along the row) then x pass (7 rows) in registers, per layer
+    for (int kk = wave; kk < HK; kk += 4) {
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            T ey[HX], iy[HX];
+#pragma unroll
+            for (int a = 0; a < HX; ++a) {
+                const T* rw = s_in + (kk * HX + a) * RW + j;
+                T e = 0, g = 0;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) {
+                    const T x = rw[t];
+                    e += k.ge[t] * x;
+                    g += k.gi[t] * x;
+                }
+                ey[a] = e;
+                iy[a] = g;
+            }
+#pragma unroll
+            for (int i = 0; i < BX; ++i) {
+                T e = 0, g = 0;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) {
+                    e += k.ge[t] * ey[i + t];
+                    g += k.gi[t] * iy[i + t];
+                }
+                s_e[(kk * BX + i) * YP + j] = e;
+                s_i[(kk * BX + i) * YP + j] = g;
+            }
+        }
+    }
+    __syncthreads();
+
+    // theta pass + relu(v - inhib) (posecell_network.py:339-340) + partial sum
+    double sum = 0.0;
+    for (int row = wave; row < BK * BX; row += 4) {
+        const int kq = row / BX, i = row - kq * BX;
+        const int gk = k0 + kq, gi = i0 + i;
+        if (gk >= TH || gi >= X) continue;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            T e = 0, g = 0;
+#pragma unroll
+            for (int t = 0; t < FL; ++t) {
+                e += k.ge[t] * s_e[((kq + t) * BX + i) * YP + j];
+                g += k.gi[t] * s_i[((kq + t) * BX + i) * YP + j];
+            }
+            const T val = (e - g) * k.scale;
+            const T q = (val < k.inhib) ? T(0) : val - k.inhib;
+            Q[((size_t)gk * X + gi) * Y + j] = q;
+            sum += (double)q;
+        }
+    }
+    sum = block_sum(sum, s_red);
+    if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+}
+
+template <typename T, int YP>
+__global__ __launch_bounds__(NT) void pc_path_rows(
+    const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
+    const T* __restrict__ filt, const int* __restrict__ ctl_ox, const int* __restrict__ ctl_oy,
+    const int* __restrict__ ctl_f, const double* __restrict__ ctl_zf,
+    unsigned long long* __restrict__ res_slot, T* __restrict__ bmax, unsigned* __restrict__ bidx,
+    int X, int Y, int TH) {
+    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF;
+    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = (NR + 3) / 4;
+    __shared__ T s_win[NR * RW];
+    __shared__ T s_r[HK * BX * YP];
+    __shared__ T s_f[HK * FT];
+    __shared__ int s_ox[HK], s_oy[HK];
+    __shared__ T s_zf[FL];
+    __shared__ double s_red[NT / 64];
+    __shared__ T s_bv[NT / 64];
+    __shared__ unsigned s_bl[NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
+
+    double tot = 0.0;
+    for (int i = tid; i < npart; i += NT) tot += part[i];
+    tot = block_sum(tot, s_red);
+    if (tid < HK) {
+        const int L = wrap_small(k0 - HALF + tid, TH);
+        s_ox[tid] = rs::wrapi(ctl_ox[L], X);   // shifts may exceed the grid (vtrans large)
+        s_oy[tid] = rs::wrapi(ctl_oy[L], Y);
+    }
+    if (tid < FL) s_zf[tid] = (T)ctl_zf[tid];
+    for (int idx = tid; idx < HK * FT; idx += NT) {
+        const int kk = idx / FT, tap = idx - kk * FT;
+        s_f[idx] = filt[ctl_f[wrap_small(k0 - HALF + kk, TH)] * FT + tap];
+    }
+    __syncthreads();
+
+    // shifted window rows: s_win[kk][a][HALF + d] = Q[L][(i0-3+a+ox) % X][(d + oy) % Y]
+    T v[RPW][JC];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int row = wave + 4 * q;
+        const int kk = row < NR ? row / HX : 0, a = row - kk * HX;
+        const int L = wrap_small(k0 - HALF + kk, TH);
+        const int r = wrap_small(i0 - HALF + a + s_ox[kk], X);
+        const T* src = Q + ((size_t)L * X + r) * Y;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int c = lane + 64 * jc;
+            v[q][jc] = (row < NR && c < Y) ? src[c] : T(0);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int row = wave + 4 * q;
+        if (row >= NR) continue;
+        const int kk = row / HX;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int c = lane + 64 * jc;
+            if (c >= Y) continue;
+            int d = c - s_oy[kk];
+            if (d < 0) d += Y;
+            T* dst = s_win + row * RW;
+            dst[HALF + d] = v[q][jc];
+            if (d < HALF) dst[HALF + Y + d] = v[q][jc];
+            if (d >= Y - HALF) dst[d - (Y - HALF)] = v[q][jc];
+        }
+    }
+    __syncthreads();
+
+    // 7x7 per-layer correlation (:273-274), register-blocked over the BX rows, clamp (:300)
+    for (int kk = wave; kk < HK; kk += 4) {
+        T f[FT];
+#pragma unroll
+        for (int t = 0; t < FT; ++t) f[t] = s_f[kk * FT + t];
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            T acc[BX];
+#pragma unroll
+            for (int i = 0; i < BX; ++i) acc[i] = 0;
+#pragma unroll
+            for (int a = 0; a < HX; ++a) {
+                T w[FL];
+                const T* rw = s_win + (kk * HX + a) * RW + j;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) w[t] = rw[t];
+#pragma unroll
+                for (int i = 0; i < BX; ++i) {
+                    const int x = a - i;
+                    if (x < 0 || x >= FL) continue;
+#pragma unroll
+                    for (int t = 0; t < FL; ++t) acc[i] += w[t] * f[x * FL + t];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < BX; ++i) s_r[(kk * BX + i) * YP + j] = acc[i] > T(0) ? acc[i] : T(0);
+        }
+    }
+    __syncthreads();
+
+    // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319)
+    unsigned long long best = 0ull;
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    const T tt = (T)tot;
+    for (int row = wave; row < BK * BX; row += 4) {
+        const int kq = row / BX, i = row - kq * BX;
+        const int gk = k0 + kq, gi = i0 + i;
+        if (gk >= TH || gi >= X) continue;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            T acc = 0;
+#pragma unroll
+            for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * s_zf[z];
+            T val = acc > T(0) ? acc : T(0);
+            if (tot != 0.0) val = val / tt;
+            P[((size_t)gk * X + gi) * Y + j] = val;
+            const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
+            if constexpr (sizeof(T) == 4) {
+                const unsigned long long key = argmax_key((float)val, lin);
+                best = key > best ? key : best;
+            } else {
+                if (val > bv || (val == bv && lin < bl)) {
+                    bv = val;
+                    bl = lin;
+                }
+            }
+        }
+    }
+    if constexpr (sizeof(T) == 4) {
+        best = wave_max_u64(best);
+        if (lane == 0) atomicMax(res_slot, best);
+    } else {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const T ov = __shfl_xor(bv, off);
+            const unsigned ol = __shfl_xor(bl, off);
+            if (ov > bv || (ov == bv && ol < bl)) {
+                bv = ov;
+                bl = ol;
+            }
+        }
+        if (lane == 0) {
+            s_bv[wave] = bv;
+            s_bl[wave] = bl;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < NT / 64; ++w)
+                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                    bv = s_bv[w];
+                    bl = s_bl[w];
+                }
+            const int b = blockIdx.y * gridDim.x + blockIdx.x;
+            bmax[b] = bv;
+            bidx[b] = bl;
+        }
+    }
+}
+
 // One block reduces per-block (value, index) argmax partials into the packed slot.
 template <typename T>
 __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ bmax,
@@ -451,6 +737,7 @@ struct rs_pc {
     bool profiling = false;
     std::vector<hipEvent_t> evPool;
     double kernelMs[2] = {0.0, 0.0};
+    int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
 };
 
 namespace {
@@ -519,23 +806,49 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
     T* Q = static_cast<T*>(h->dQ);
     const SepKernel<T>& k = sep_of<T>(h);
     unsigned long long* slot = h->dRes + s;
-    dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX, (h->TH + EX_BK - 1) / EX_BK);
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
-    hipLaunchKernelGGL((pc_excite_kernel<T, EX_BX, EX_BY, EX_BK>), gA, dim3(NT), 0, h->stream, P, Q,
-                       h->dPart, slot, h->X, h->Y, h->TH, k);
-    RS_HIP(hipGetLastError());
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
-    if (excite_only) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
     const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
-    dim3 gB((h->Y + PI_BY - 1) / PI_BY, (h->X + PI_BX - 1) / PI_BX, (h->TH + PI_BK - 1) / PI_BK);
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
-    hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
-                       static_cast<T*>(h->dP), h->dPart, h->nPart,
-                       static_cast<const T*>(h->dFilt), reinterpret_cast<const int*>(rec),
-                       reinterpret_cast<const int*>(rec + ctl_off_oy(h)),
-                       reinterpret_cast<const int*>(rec + ctl_off_f(h)),
-                       reinterpret_cast<const double*>(rec + ctl_off_zf(h)), slot,
-                       static_cast<T*>(h->dBmax), h->dBidx, h->X, h->Y, h->TH);
+    const int* cox = reinterpret_cast<const int*>(rec);
+    const int* coy = reinterpret_cast<const int*>(rec + ctl_off_oy(h));
+    const int* cf = reinterpret_cast<const int*>(rec + ctl_off_f(h));
+    const double* czf = reinterpret_cast<const double*>(rec + ctl_off_zf(h));
+    T* bmax = static_cast<T*>(h->dBmax);
+    const T* filt = static_cast<const T*>(h->dFilt);
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
+    if (h->tiling == 64 || h->tiling == 128) {
+        const dim3 g((h->X + RT_BX - 1) / RT_BX, (h->TH + RT_BK - 1) / RT_BK);
+        if (h->tiling == 64)
+            hipLaunchKernelGGL((pc_excite_rows<T, 64>), g, dim3(NT), 0, h->stream, P, Q, h->dPart,
+                               slot, h->X, h->Y, h->TH, k);
+        else
+            hipLaunchKernelGGL((pc_excite_rows<T, 128>), g, dim3(NT), 0, h->stream, P, Q, h->dPart,
+                               slot, h->X, h->Y, h->TH, k);
+        RS_HIP(hipGetLastError());
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+        if (excite_only) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+        if (h->tiling == 64)
+            hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(NT), 0, h->stream, Q,
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
+                               slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+        else
+            hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(NT), 0, h->stream, Q,
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
+                               slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+    } else {
+        const dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX,
+                      (h->TH + EX_BK - 1) / EX_BK);
+        hipLaunchKernelGGL((pc_excite_kernel<T, EX_BX, EX_BY, EX_BK>), gA, dim3(NT), 0, h->stream,
+                           P, Q, h->dPart, slot, h->X, h->Y, h->TH, k);
+        RS_HIP(hipGetLastError());
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+        if (excite_only) return RS_OK;
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+        const dim3 gB((h->Y + PI_BY - 1) / PI_BY, (h->X + PI_BX - 1) / PI_BX,
+                      (h->TH + PI_BK - 1) / PI_BK);
+        hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
+                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
+                           slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+    }
     RS_HIP(hipGetLastError());
     if (sizeof(T) == 8) {
         hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
@@ -665,9 +978,15 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     fill_sep(h->kf, p);
     fill_sep(h->kd, p);
     h->ctlStride = rs::round_up(ctl_off_zf(h) + sizeof(double) * 8, 16);
-    h->nPart = ((Y + EX_BY - 1) / EX_BY) * ((X + EX_BX - 1) / EX_BX) * ((TH + EX_BK - 1) / EX_BK);
-    h->nPathBlocks =
-        ((Y + PI_BY - 1) / PI_BY) * ((X + PI_BX - 1) / PI_BX) * ((TH + PI_BK - 1) / PI_BK);
+    h->tiling = Y <= 64 ? 64 : (Y <= 128 ? 128 : 0);
+    if (h->tiling) {
+        h->nPart = ((X + RT_BX - 1) / RT_BX) * ((TH + RT_BK - 1) / RT_BK);
+        h->nPathBlocks = h->nPart;
+    } else {
+        h->nPart = ((Y + EX_BY - 1) / EX_BY) * ((X + EX_BX - 1) / EX_BX) * ((TH + EX_BK - 1) / EX_BK);
+        h->nPathBlocks =
+            ((Y + PI_BY - 1) / PI_BY) * ((X + PI_BX - 1) / PI_BX) * ((TH + PI_BK - 1) / PI_BK);
+    }
     h->nBmaxCap = h->nPathBlocks > 1024 ? h->nPathBlocks : 1024;
 
     auto fail = [&](int code) { rs_pc_destroy(h); return code; };
