@@ -63,21 +63,6 @@ __device__ inline double block_sum(double v, double* s_red) {
     return t;
 }
 
-__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        unsigned long long o = __shfl_xor(v, off);
-        v = o > v ? o : v;
-    }
-    return v;
-}
-
-// Packed argmax key for non-negative float values: larger value wins, then the
-// smaller reference linear index (numpy argmax returns the first maximum).
-__device__ inline unsigned long long argmax_key(float v, unsigned lin) {
-    return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
-}
-
 // ---------------------------------------------------------------------------
 // Kernel 1: excitation (3-D DoG, separable) + global inhibition + partial sums
 // posecell_network.py:336-343 (conv -> inhibit -> sum)
@@ -97,8 +82,6 @@ __global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, 
 
     const int tid = threadIdx.x;
     const int j0 = blockIdx.x * BY, i0 = blockIdx.y * BX, k0 = blockIdx.z * BK;
-    if (res_slot != nullptr && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
-        *res_slot = 0ull;  // the path kernel of this step max-reduces into it
 
     for (int idx = tid; idx < HK * HX * HY; idx += NT) {
         const int kk = idx / (HX * HY);
@@ -239,7 +222,6 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
     __syncthreads();
 
     // theta filter, clamp (:310-314), normalise, store, argmax
-    unsigned long long best = 0ull;
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
     const T tt = (T)tot;
@@ -256,22 +238,15 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
             if (tot != 0.0) v = v / tt;
             P[((size_t)gk * X + gi) * Y + gj] = v;
             const unsigned lin = ((unsigned)gi * Y + gj) * TH + gk;
-            if constexpr (sizeof(T) == 4) {
-                const unsigned long long key = argmax_key((float)v, lin);
-                best = key > best ? key : best;
-            } else {
-                if (v > bv || (v == bv && lin < bl)) {
-                    bv = v;
-                    bl = lin;
-                }
+            if (v > bv || (v == bv && lin < bl)) {
+                bv = v;
+                bl = lin;
             }
         }
     }
-    if constexpr (sizeof(T) == 4) {
-        best = wave_max_u64(best);
-        if ((tid & 63) == 0) atomicMax(res_slot, best);
-    } else {
-        // wave argmax, then block argmax, one (value, index) per block
+    {
+        // wave argmax, then block argmax: one (value, index) partial per block,
+        // reduced per step by pc_argmax_steps (no same-address atomics)
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const T ov = __shfl_xor(bv, off);
@@ -329,8 +304,6 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
     __shared__ double s_red[NT / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
-    if (res_slot != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0)
-        *res_slot = 0ull;  // the path kernel of this step max-reduces into it
 
     T v[RPW][JC];
 #pragma unroll
@@ -524,7 +497,6 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
     __syncthreads();
 
     // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319)
-    unsigned long long best = 0ull;
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
     const T tt = (T)tot;
@@ -543,21 +515,13 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
             if (tot != 0.0) val = val / tt;
             P[((size_t)gk * X + gi) * Y + j] = val;
             const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
-            if constexpr (sizeof(T) == 4) {
-                const unsigned long long key = argmax_key((float)val, lin);
-                best = key > best ? key : best;
-            } else {
-                if (val > bv || (val == bv && lin < bl)) {
-                    bv = val;
-                    bl = lin;
-                }
+            if (val > bv || (val == bv && lin < bl)) {
+                bv = val;
+                bl = lin;
             }
         }
     }
-    if constexpr (sizeof(T) == 4) {
-        best = wave_max_u64(best);
-        if (lane == 0) atomicMax(res_slot, best);
-    } else {
+    {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const T ov = __shfl_xor(bv, off);
@@ -617,6 +581,41 @@ __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ b
         __syncthreads();
     }
     if (threadIdx.x == 0) *res_slot = 0xFFFFFFFFull - s_bl[0];  // same decoding as the packed key
+}
+
+// Per-step argmax: block s reduces the nb (value, index) partials of step s.
+template <typename T>
+__global__ __launch_bounds__(NT) void pc_argmax_steps(const T* __restrict__ bmax,
+                                                      const unsigned* __restrict__ bidx, int nb,
+                                                      unsigned long long* __restrict__ res) {
+    __shared__ T s_bv[NT];
+    __shared__ unsigned s_bl[NT];
+    const size_t base = (size_t)blockIdx.x * nb;
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    for (int i = threadIdx.x; i < nb; i += NT) {
+        const T v = bmax[base + i];
+        const unsigned l = bidx[base + i];
+        if (v > bv || (v == bv && l < bl)) {
+            bv = v;
+            bl = l;
+        }
+    }
+    s_bv[threadIdx.x] = bv;
+    s_bl[threadIdx.x] = bl;
+    __syncthreads();
+    for (int st = NT / 2; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            const T v = s_bv[threadIdx.x + st];
+            const unsigned l = s_bl[threadIdx.x + st];
+            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+                s_bv[threadIdx.x] = v;
+                s_bl[threadIdx.x] = l;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) res[blockIdx.x] = 0xFFFFFFFFull - s_bl[0];
 }
 
 // Argmax of the stored state (get_pc_max outside update): per-block partials.
@@ -723,6 +722,8 @@ struct rs_pc {
     int nBmaxCap = 0;
     unsigned long long* dRes = nullptr;
     int resCap = 0;
+    void* dArgV = nullptr;        // per-step per-block argmax partials [resCap][nPathBlocks]
+    unsigned* dArgI = nullptr;
     unsigned long long* hRes = nullptr;  // pinned
     unsigned char* dCtl = nullptr;
     unsigned char* hCtl = nullptr;       // pinned
@@ -750,11 +751,16 @@ int pc_grow_steps(rs_pc* h, int n) {
     if (h->hCtl) RS_HIP(hipHostFree(h->hCtl));
     if (h->dRes) RS_HIP(hipFree(h->dRes));
     if (h->hRes) RS_HIP(hipHostFree(h->hRes));
+    if (h->dArgV) RS_HIP(hipFree(h->dArgV));
+    if (h->dArgI) RS_HIP(hipFree(h->dArgI));
     h->dCtl = nullptr; h->hCtl = nullptr; h->dRes = nullptr; h->hRes = nullptr;
+    h->dArgV = nullptr; h->dArgI = nullptr;
     RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
     RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * cap));
     RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap, hipHostMallocDefault));
+    RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
+    RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
     h->ctlCap = cap;
     h->resCap = cap;
     return RS_OK;
@@ -811,7 +817,8 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
     const int* coy = reinterpret_cast<const int*>(rec + ctl_off_oy(h));
     const int* cf = reinterpret_cast<const int*>(rec + ctl_off_f(h));
     const double* czf = reinterpret_cast<const double*>(rec + ctl_off_zf(h));
-    T* bmax = static_cast<T*>(h->dBmax);
+    T* bmax = static_cast<T*>(h->dArgV) + (size_t)s * h->nPathBlocks;
+    unsigned* bidx = h->dArgI + (size_t)s * h->nPathBlocks;
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->tiling == 64 || h->tiling == 128) {
@@ -829,11 +836,11 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
         if (h->tiling == 64)
             hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(NT), 0, h->stream, Q,
                                static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                               slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+                               slot, bmax, bidx, h->X, h->Y, h->TH);
         else
             hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(NT), 0, h->stream, Q,
                                static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                               slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+                               slot, bmax, bidx, h->X, h->Y, h->TH);
     } else {
         const dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX,
                       (h->TH + EX_BK - 1) / EX_BK);
@@ -847,14 +854,9 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
                       (h->TH + PI_BK - 1) / PI_BK);
         hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
                            static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                           slot, bmax, h->dBidx, h->X, h->Y, h->TH);
+                           slot, bmax, bidx, h->X, h->Y, h->TH);
     }
     RS_HIP(hipGetLastError());
-    if (sizeof(T) == 8) {
-        hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
-                           static_cast<const T*>(h->dBmax), h->dBidx, h->nPathBlocks, slot);
-        RS_HIP(hipGetLastError());
-    }
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 3], h->stream));
     return RS_OK;
 }
@@ -885,6 +887,13 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         else
             RS_TRY(pc_launch_step<double>(h, s, false, pb));
     }
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_argmax_steps<float>), dim3(n), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
+    else
+        hipLaunchKernelGGL((pc_argmax_steps<double>), dim3(n), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
+    RS_HIP(hipGetLastError());
     RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost,
                           h->stream));
@@ -1035,7 +1044,8 @@ int rs_pc_destroy(rs_pc* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx,
+    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
+                    (void*)h->dArgI,
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
         if (p) (void)hipFree(p);
     if (h->hRes) (void)hipHostFree(h->hRes);

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -79,15 +80,17 @@ __global__ void vt_store_kernel(const uint8_t* __restrict__ raw, const int32_t* 
     }
 }
 
-// Query forms: qf[(n*WD + c)*H + r] = (cL, cH) of c = -Q[r][4c..4c+3] mod 256.
-__global__ void vt_qform_kernel(const uint8_t* __restrict__ raw, int n, int H, int W, int WD,
-                                uint2* __restrict__ qf) {
-    const int64_t total = (int64_t)n * WD * H;
-    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int qn = (int)(idx / ((int64_t)WD * H));
-        const int rem = (int)(idx - (int64_t)qn * WD * H);
-        const int c = rem / H, r = rem - c * H;
+// Query forms: qf[(n*WD + c)*H + r] = (cL, cH) of c = -Q[r][4c..4c+3] mod 256,
+// and qsum[n] = sum over rows [M, H-M) of the bytes of c (carry-count scan).
+// One block per query.
+__global__ __launch_bounds__(256) void vt_qform_kernel(const uint8_t* __restrict__ raw, int H, int W,
+                                                       int WD, int M, uint2* __restrict__ qf,
+                                                       uint32_t* __restrict__ qsum) {
+    __shared__ uint32_t s_red[4];
+    const int qn = blockIdx.x;
+    uint32_t part = 0;
+    for (int idx = threadIdx.x; idx < WD * H; idx += blockDim.x) {
+        const int c = idx / H, r = idx - c * H;
         uint32_t neg = 0;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -95,8 +98,14 @@ __global__ void vt_qform_kernel(const uint8_t* __restrict__ raw, int n, int H, i
             const uint32_t byte = col < W ? raw[((size_t)qn * H + r) * W + col] : 0u;
             neg |= ((256u - byte) & 0xFFu) << (8 * b);
         }
-        qf[idx] = make_uint2(neg & 0x7F7F7F7Fu, neg & 0x80808080u);
+        qf[(size_t)qn * WD * H + idx] = make_uint2(neg & 0x7F7F7F7Fu, neg & 0x80808080u);
+        if (r >= M && r < H - M) part = __builtin_amdgcn_sad_u8(neg, 0u, part);
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) qsum[qn] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
 }
 
 // Output of a scan: either min-reduce packed keys per query (best[]) or
@@ -240,6 +249,163 @@ __global__ __launch_bounds__(64) void vt_scan_col_kernel(const uint4* __restrict
     }
 }
 
+// --- carry-count forms.  v_sad_u8 issues at half rate on gfx950 (measured,
+// tools/ubench_valu.hip), so the byte sum is taken apart exactly:
+//   sum_b (a_b + c_b) mod 256 = bytesum(a) + bytesum(c) - 256 * #carries,
+// with the carry out of byte b = majority(a_b7, c_b7, bit 7 of (a&0x7f + c&0x7f)_b):
+// one v_bitop3 (table 0xE8; zero outside bit 7 since aH, cH are), counted by
+// v_bcnt_u32_b32.  Per pair: v_add_u32 + v_bitop3_b32 + v_bcnt_u32_b32, all full
+// rate.  bytesum(a) over each offset's row window is a sliding sum per column
+// (query-independent), bytesum(c) is qsum[] from vt_qform_kernel.
+__device__ inline uint32_t carry_pair(uint32_t aL, uint32_t aH, uint2 f, uint32_t cnt) {
+    return __builtin_popcount(__builtin_amdgcn_bitop3_b32(aH, f.y, aL + f.x, 0xE8)) + cnt;
+}
+
+template <int H, int NQ, bool MATRIX>
+__global__ __launch_bounds__(64) void vt_scan_carry_kernel(const uint4* __restrict__ lib, int ntb,
+                                                           int64_t count, int WD,
+                                                           const uint2* __restrict__ qf,
+                                                           const uint32_t* __restrict__ qsum,
+                                                           int nq, ScanOut out, int rank,
+                                                           int nranks) {
+    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1, R0 = M, R1 = H - M;
+    const int tb = blockIdx.x % ntb;
+    const int qbase = (blockIdx.x / ntb) * NQ;
+    const int lane = threadIdx.x;
+    uint32_t cnt[NQ][NO];
+    uint32_t A[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+        A[o] = 0u;
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) cnt[n][o] = 0u;
+    }
+    for (int c = 0; c < WD; ++c) {
+        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + lane;
+        uint32_t aL[4 * HQ], aH[4 * HQ], bs[4 * HQ];
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+            const uint4 v = col[(size_t)q * 64];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
+                aH[4 * q + k] = w[k] & 0x80808080u;
+                bs[4 * q + k] = __builtin_amdgcn_sad_u8(w[k], 0u, 0u);
+            }
+        }
+        uint32_t win = 0u;
+#pragma unroll
+        for (int s = R0 - (M - 1); s < R1 - (M - 1); ++s) win += bs[s];
+        A[0] += win;
+#pragma unroll
+        for (int o = 1; o < NO; ++o) {
+            win += bs[R1 - (M - 1) + o - 1] - bs[R0 - (M - 1) + o - 1];
+            A[o] += win;
+        }
+#pragma unroll
+        for (int r = R0; r < R1; ++r) {
+#pragma unroll
+            for (int n = 0; n < NQ; ++n) {
+                const int qi = min(qbase + n, nq - 1);
+                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
+#pragma unroll
+                for (int o = 0; o < NO; ++o) {
+                    const int s = r + o - (M - 1);
+                    cnt[n][o] = carry_pair(aL[s], aH[s], f, cnt[n][o]);
+                }
+            }
+        }
+    }
+    const int64_t slot = (int64_t)tb * 64 + lane;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+        const uint32_t qs = qsum[min(qbase + n, nq - 1)];
+        uint32_t sc = 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) sc = min(sc, A[o] + qs - 256u * cnt[n][o]);
+        emit_score<MATRIX>(out, slot, count, qbase + n, nq, sc, rank, nranks, lane == 0);
+    }
+}
+
+template <int H, int NQ>
+__global__ __launch_bounds__(64) void vt_scan_carry_col_kernel(const uint4* __restrict__ lib,
+                                                               int64_t count, int WD,
+                                                               const uint2* __restrict__ qf,
+                                                               const uint32_t* __restrict__ qsum,
+                                                               int nq, ScanOut out, int rank,
+                                                               int nranks) {
+    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1, R0 = M, R1 = H - M;
+    const int lane = threadIdx.x;
+    const int t8 = lane >> 3, cl = lane & 7;
+    const int64_t slot = (int64_t)blockIdx.x * 8 + t8;
+    const int64_t tb = slot >> 6, tl = slot & 63;
+    const int qbase = blockIdx.y * NQ;
+    uint32_t val[NQ][NO];  // bytesum(a) - 256 * carries, mod 2^32, this lane's columns
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) val[n][o] = 0u;
+    for (int c = cl; c < WD; c += 8) {
+        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + tl;
+        uint32_t aL[4 * HQ], aH[4 * HQ], bs[4 * HQ];
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+            const uint4 v = col[(size_t)q * 64];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
+                aH[4 * q + k] = w[k] & 0x80808080u;
+                bs[4 * q + k] = __builtin_amdgcn_sad_u8(w[k], 0u, 0u);
+            }
+        }
+        uint32_t A[NO];
+        uint32_t win = 0u;
+#pragma unroll
+        for (int s = R0 - (M - 1); s < R1 - (M - 1); ++s) win += bs[s];
+        A[0] = win;
+#pragma unroll
+        for (int o = 1; o < NO; ++o) {
+            win += bs[R1 - (M - 1) + o - 1] - bs[R0 - (M - 1) + o - 1];
+            A[o] = win;
+        }
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+            uint32_t cnt[NO];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) cnt[o] = 0u;
+            const int qi = min(qbase + n, nq - 1);
+#pragma unroll
+            for (int r = R0; r < R1; ++r) {
+                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
+#pragma unroll
+                for (int o = 0; o < NO; ++o) cnt[o] = carry_pair(aL[r + o - (M - 1)], aH[r + o - (M - 1)], f, cnt[o]);
+            }
+#pragma unroll
+            for (int o = 0; o < NO; ++o) val[n][o] += A[o] - 256u * cnt[o];
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+        const uint32_t qs = qsum[min(qbase + n, nq - 1)];
+        uint32_t sc = 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+            uint32_t v = val[n][o];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            sc = min(sc, v + qs);
+        }
+        const unsigned long long g = (unsigned long long)slot * nranks + rank;
+        unsigned long long key =
+            (slot < count && cl == 0) ? (((unsigned long long)sc << 32) | g) : NO_KEY;
+        key = wave_min_u64(key);
+        if (lane == 0 && qbase + n < nq) atomicMin(out.best + qbase + n, key);
+    }
+}
+
 // --- generic form (any H, max_offset): one thread per (slot, query).
 template <bool MATRIX>
 __global__ __launch_bounds__(64) void vt_scan_generic_kernel(const uint4* __restrict__ lib, int ntb,
@@ -291,6 +457,7 @@ struct rs_vt {
     uint8_t* dQraw = nullptr;
     uint8_t* hQraw = nullptr;  // pinned
     uint2* dQf = nullptr;
+    uint32_t* dQsum = nullptr;
     unsigned long long* dBest = nullptr;
     unsigned long long* hBest = nullptr;  // pinned
     // index lists for stores
@@ -308,6 +475,7 @@ struct rs_vt {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
+    bool carry = true;  // carry-count scan (default) or v_sad_u8 scan (RS_VT_SCAN=sad)
 };
 
 namespace {
@@ -351,12 +519,14 @@ int vt_grow_queries(rs_vt* h, int nq) {
     if (h->dQraw) RS_HIP(hipFree(h->dQraw));
     if (h->hQraw) RS_HIP(hipHostFree(h->hQraw));
     if (h->dQf) RS_HIP(hipFree(h->dQf));
+    if (h->dQsum) RS_HIP(hipFree(h->dQsum));
     if (h->dBest) RS_HIP(hipFree(h->dBest));
     if (h->hBest) RS_HIP(hipHostFree(h->hBest));
     const size_t qb = (size_t)h->H * h->W;
     RS_HIP(hipMalloc(&h->dQraw, qb * cap));
     RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dQf, sizeof(uint2) * (size_t)h->WD * h->H * cap));
+    RS_HIP(hipMalloc(&h->dQsum, sizeof(uint32_t) * cap));
     RS_HIP(hipMalloc(&h->dBest, sizeof(unsigned long long) * cap));
     RS_HIP(hipHostMalloc(&h->hBest, sizeof(unsigned long long) * cap, hipHostMallocDefault));
     h->qCap = cap;
@@ -407,10 +577,8 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     const size_t qb = (size_t)h->H * h->W * nq;
     std::memcpy(h->hQraw, queries, qb);
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
-    const int64_t total = (int64_t)nq * h->WD * h->H;
-    const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(vt_qform_kernel, dim3(grid), dim3(256), 0, h->stream, h->dQraw, nq, h->H,
-                       h->W, h->WD, h->dQf);
+    hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H, h->W,
+                       h->WD, h->M, h->dQf, h->dQsum);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
@@ -439,22 +607,41 @@ int vt_launch_scan(rs_vt* h, const uint4* lib, int64_t count, int nq, ScanOut ou
     if (fast && !MATRIX && (int64_t)ntb * nq < 2048 && h->WD <= 8) {
         // few waves of work: spread each template over 8 column lanes
         const int nb8 = (int)((count + 7) / 8);
-        if (h->H == 64)
-            hipLaunchKernelGGL((vt_scan_col_kernel<64, 1>), dim3(nb8, nq), dim3(64), 0, h->stream,
-                               lib, count, h->WD, h->dQf, nq, out, rank, nranks);
-        else
-            hipLaunchKernelGGL((vt_scan_col_kernel<32, 1>), dim3(nb8, nq), dim3(64), 0, h->stream,
-                               lib, count, h->WD, h->dQf, nq, out, rank, nranks);
+        const dim3 grid(nb8, nq);
+        if (h->carry) {
+            if (h->H == 64)
+                hipLaunchKernelGGL((vt_scan_carry_col_kernel<64, 1>), grid, dim3(64), 0, h->stream,
+                                   lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
+            else
+                hipLaunchKernelGGL((vt_scan_carry_col_kernel<32, 1>), grid, dim3(64), 0, h->stream,
+                                   lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
+        } else if (h->H == 64) {
+            hipLaunchKernelGGL((vt_scan_col_kernel<64, 1>), grid, dim3(64), 0, h->stream, lib,
+                               count, h->WD, h->dQf, nq, out, rank, nranks);
+        } else {
+            hipLaunchKernelGGL((vt_scan_col_kernel<32, 1>), grid, dim3(64), 0, h->stream, lib,
+                               count, h->WD, h->dQf, nq, out, rank, nranks);
+        }
     } else if (fast) {
         constexpr int NQ = 2;
         const int nqg = (nq + NQ - 1) / NQ;
         const dim3 grid((unsigned)(ntb * nqg));
-        if (h->H == 64)
+        if (h->carry) {
+            if (h->H == 64)
+                hipLaunchKernelGGL((vt_scan_carry_kernel<64, NQ, MATRIX>), grid, dim3(64), 0,
+                                   h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
+                                   rank, nranks);
+            else
+                hipLaunchKernelGGL((vt_scan_carry_kernel<32, NQ, MATRIX>), grid, dim3(64), 0,
+                                   h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
+                                   rank, nranks);
+        } else if (h->H == 64) {
             hipLaunchKernelGGL((vt_scan_lane_kernel<64, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
                                lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        else
+        } else {
             hipLaunchKernelGGL((vt_scan_lane_kernel<32, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
                                lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+        }
     } else {
         hipLaunchKernelGGL((vt_scan_generic_kernel<MATRIX>), dim3((unsigned)(ntb * nq)), dim3(64),
                            0, h->stream, lib, ntb, count, h->H, h->M, h->WD, h->dQf, nq, out, rank,
@@ -623,6 +810,7 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
     h->H = H; h->W = W; h->M = max_offset; h->thr = thr; h->device = device;
     h->WD = (W + 3) / 4;
     h->HQ = (H + 3) / 4;
+    if (const char* e = std::getenv("RS_VT_SCAN")) h->carry = std::strcmp(e, "sad") != 0;
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
@@ -647,7 +835,7 @@ int rs_vt_destroy(rs_vt* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
-    for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dBest,
+    for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat})

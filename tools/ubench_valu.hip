@@ -29,6 +29,12 @@ constexpr int ITERS = 4096;
 #define BOP3(r) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r) : "v"(x), "v"(y))
 #define XOR(r) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(r) : "v"(x))
 #define DOT4(r) asm volatile("v_dot4_u32_u8 %0, %1, %2, %0" : "+v"(r) : "v"(x), "v"(y))
+#define BCNT(r) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(r) : "v"(x))
+#define ADD3(r) asm volatile("v_add3_u32 %0, %1, %2, %0" : "+v"(r) : "v"(x), "v"(y))
+#define PERM(r) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(r) : "v"(x), "v"(y))
+#define CARRY(r)                                                                     \
+    asm volatile("v_add_u32 %0, %1, %0\n\tv_bitop3_b32 %0, %1, %2, %0 bitop3:0xe8\n\t" \
+                 "v_bcnt_u32_b32 %0, %0, %0" : "+v"(r) : "v"(x), "v"(y))
 #define MIX(r)                                                                       \
     asm volatile("v_add_u32 %0, %1, %0\n\tv_bitop3_b32 %0, %0, %1, %2 bitop3:0x96\n\t" \
                  "v_sad_u8 %0, %0, 0, %0" : "+v"(r) : "v"(x), "v"(y))
@@ -43,6 +49,10 @@ __global__ void ubench(unsigned* out, unsigned x, unsigned y) {
     if (K == 3) CHAIN8(XOR)
     if (K == 4) CHAIN8(DOT4)
     if (K == 5) CHAIN8(MIX)
+    if (K == 6) CHAIN8(BCNT)
+    if (K == 7) CHAIN8(ADD3)
+    if (K == 8) CHAIN8(PERM)
+    if (K == 9) CHAIN8(CARRY)
     out[blockIdx.x * blockDim.x + threadIdx.x] = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
 }
 
@@ -76,13 +86,15 @@ void run(const char* name, int insn_per_body, int waves_per_simd) {
 }
 
 int main() {
-    for (int w : {1, 2, 4, 8}) {
+    for (int w : {2, 4, 8}) {
         run<0>("sad_u8", 1, w);
         run<1>("add_u32", 1, w);
         run<2>("bitop3", 1, w);
-        run<3>("xor", 1, w);
-        run<4>("dot4", 1, w);
+        run<6>("bcnt", 1, w);
+        run<7>("add3", 1, w);
+        run<8>("perm", 1, w);
         run<5>("mix3", 3, w);
+        run<9>("carry3", 3, w);
     }
     return 0;
 }
