@@ -45,6 +45,22 @@ struct SepKernel {
     T inhib;
 };
 
+// Phase stamps for the diagnostic probe (tools/pc_probe.hip defines PC_STAMPS);
+// compiled out of the library.
+#ifdef PC_STAMPS
+#define PC_STAMP(kid, sid)                                                              \
+    do {                                                                                \
+        if (threadIdx.x == 0) {                                                         \
+            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                    \
+            pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                               \
+    } while (0)
+#else
+#define PC_STAMP(kid, sid) \
+    do {                   \
+    } while (0)
+#endif
+
 // Tile shapes (output cells per block = BK layers x BX rows x BY cols).
 constexpr int EX_BX = 8, EX_BY = 16, EX_BK = 4;
 constexpr int PI_BX = 8, PI_BY = 16, PI_BK = 4;
@@ -304,6 +320,7 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
     __shared__ double s_red[NT / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
+    PC_STAMP(0, 0);
 
     T v[RPW][JC];
 #pragma unroll
@@ -333,6 +350,7 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
         }
     }
     __syncthreads();
+    PC_STAMP(0, 1);
 
     // y pass (7 taps along the row) then x pass (7 rows) in registers, per layer
     for (int kk = wave; kk < HK; kk += 4) {
@@ -368,6 +386,7 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
         }
     }
     __syncthreads();
+    PC_STAMP(0, 2);
 
     // theta pass + relu(v - inhib) (posecell_network.py:339-340) + partial sum
     double sum = 0.0;
@@ -393,6 +412,7 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
     }
     sum = block_sum(sum, s_red);
     if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    PC_STAMP(0, 3);
 }
 
 template <typename T, int YP>
@@ -414,10 +434,12 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
     __shared__ unsigned s_bl[NT / 64];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
+    PC_STAMP(1, 0);
 
     double tot = 0.0;
     for (int i = tid; i < npart; i += NT) tot += part[i];
     tot = block_sum(tot, s_red);
+    PC_STAMP(1, 1);
     if (tid < HK) {
         const int L = wrap_small(k0 - HALF + tid, TH);
         s_ox[tid] = rs::wrapi(ctl_ox[L], X);   // shifts may exceed the grid (vtrans large)
@@ -429,6 +451,7 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
         s_f[idx] = filt[ctl_f[wrap_small(k0 - HALF + kk, TH)] * FT + tap];
     }
     __syncthreads();
+    PC_STAMP(1, 2);
 
     // shifted window rows: s_win[kk][a][HALF + d] = Q[L][(i0-3+a+ox) % X][(d + oy) % Y]
     T v[RPW][JC];
@@ -463,6 +486,7 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
         }
     }
     __syncthreads();
+    PC_STAMP(1, 3);
 
     // 7x7 per-layer correlation (:273-274), register-blocked over the BX rows, clamp (:300)
     for (int kk = wave; kk < HK; kk += 4) {
@@ -495,6 +519,7 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
         }
     }
     __syncthreads();
+    PC_STAMP(1, 4);
 
     // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319)
     T bv = T(-1);
@@ -547,6 +572,7 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
             bidx[b] = bl;
         }
     }
+    PC_STAMP(1, 5);
 }
 
 // One block reduces per-block (value, index) argmax partials into the packed slot.

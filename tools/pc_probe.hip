@@ -1,0 +1,144 @@
+// Diagnostic probe for the pose-cell step kernels (not part of the library).
+// Builds posecell.hip with PC_STAMPS so the row kernels write s_memrealtime
+// stamps (100 MHz) at their phase boundaries, then reports per-phase times
+// over the blocks of one step, and back-to-back launch costs of each kernel
+// alone and of an empty kernel with the same grid.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ipyratslam_amd/csrc \
+//         tools/pc_probe.hip pyratslam_amd/csrc/rs_common.cpp -o /tmp/pc_probe
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#define PC_STAMPS 1
+__device__ unsigned long long* pc_dbg;
+#include "posecell.hip"
+
+#define CK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            return 1;                                                          \
+        }                                                                      \
+    } while (0)
+
+__global__ void empty_kernel(int* p) {
+    if (p && threadIdx.x == 1023) p[0] = 1;
+}
+
+static double median(std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0 : v[v.size() / 2];
+}
+
+int main(int argc, char** argv) {
+    int X = 64, Y = 64, TH = 36;
+    if (argc == 4) {
+        X = atoi(argv[1]);
+        Y = atoi(argv[2]);
+        TH = atoi(argv[3]);
+    }
+    rs_pc_params p{};
+    p.precision = RS_PREC_F32;
+    p.global_inhibition = 0.2;
+    double norm = 0;
+    for (int t = 0; t < 7; ++t) {
+        p.ge[t] = std::exp(-(t - 3) * (t - 3) / 2.0) / std::sqrt(2 * M_PI);
+        p.gi[t] = std::exp(-(t - 3) * (t - 3) / 8.0) / (2 * std::sqrt(2 * M_PI));
+    }
+    for (int a = 0; a < 7; ++a)
+        for (int b = 0; b < 7; ++b)
+            for (int c = 0; c < 7; ++c)
+                norm += p.ge[a] * p.ge[b] * p.ge[c] - p.gi[a] * p.gi[b] * p.gi[c];
+    p.k_scale = 1.0 / std::fabs(norm);
+    std::vector<double> filt(4 * 49, 1.0 / 49);
+    p.nfilters = 4;
+    p.xy_filters = filt.data();
+    rs_pc* h = nullptr;
+    if (rs_pc_create(X, Y, TH, &p, 0, &h) != RS_OK) {
+        fprintf(stderr, "create: %s\n", rs_last_error());
+        return 1;
+    }
+    rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
+    unsigned long long* dbg;
+    const size_t ndbg = 2 * 4096 * 8;
+    CK(hipMalloc(&dbg, ndbg * 8));
+    CK(hipMemset(dbg, 0, ndbg * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
+    const int n = 200;
+    std::vector<int32_t> ox(n * TH, 1), oy(n * TH, -1), f(n * TH, 0), out(3 * n);
+    std::vector<double> zf(n * 7, 0.1);
+    for (int s = 0; s < n; ++s) zf[s * 7 + 3] = 0.4;
+    for (int rep = 0; rep < 3; ++rep)
+        if (rs_pc_run(h, n, ox.data(), oy.data(), f.data(), zf.data(), out.data()) != RS_OK) {
+            fprintf(stderr, "run: %s\n", rs_last_error());
+            return 1;
+        }
+    double ms = 0;
+    rs_pc_last_ms(h, &ms);
+    printf("grid %dx%dx%d  tiling %d  blocks %d  run(%d): %.2f us/step\n", X, Y, TH, h->tiling,
+           h->nPart, n, 1e3 * ms / n, h->nPart);
+    // stamps of the last step
+    std::vector<unsigned long long> st(ndbg);
+    CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
+    const int nb = h->nPart;
+    for (int kid = 0; kid < 2; ++kid) {
+        const int ns = kid == 0 ? 4 : 6;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<std::vector<double>> ph(ns);
+        for (int b = 0; b < nb; ++b) {
+            const unsigned long long* r = &st[((size_t)kid * 4096 + b) * 8];
+            t0 = std::min(t0, r[0]);
+            t1 = std::max(t1, r[ns - 1]);
+            for (int i = 1; i < ns; ++i) ph[i].push_back((r[i] - r[i - 1]) * 10.0);
+            ph[0].push_back((double)r[0]);
+        }
+        std::vector<double> starts;
+        for (int b = 0; b < nb; ++b) starts.push_back((st[((size_t)kid * 4096 + b) * 8] - t0) * 10.0);
+        printf("%s: first start -> last end %.2f us; start spread median %.2f max %.2f us\n",
+               kid == 0 ? "excite" : "path", (t1 - t0) * 1e-2, median(starts) * 1e-3,
+               *std::max_element(starts.begin(), starts.end()) * 1e-3);
+        for (int i = 1; i < ns; ++i)
+            printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph[i]) * 1e-3,
+                   *std::max_element(ph[i].begin(), ph[i].end()) * 1e-3);
+    }
+    // back-to-back launch costs
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const dim3 g((X + RT_BX - 1) / RT_BX, (TH + RT_BK - 1) / RT_BK);
+    const int reps = 500;
+    float t = 0;
+    CK(hipEventRecord(e0, h->stream));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL(empty_kernel, g, dim3(256), 0, h->stream, nullptr);
+    CK(hipEventRecord(e1, h->stream));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&t, e0, e1));
+    printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
+    const unsigned char* rec = h->dCtl;
+    CK(hipEventRecord(e0, h->stream));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((pc_excite_rows<float, 64>), g, dim3(256), 0, h->stream,
+                           (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->kf);
+    CK(hipEventRecord(e1, h->stream));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&t, e0, e1));
+    printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
+    CK(hipEventRecord(e0, h->stream));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((pc_path_rows<float, 64>), g, dim3(256), 0, h->stream, (const float*)h->dQ,
+                           (float*)h->dP, h->dPart, h->nPart, (const float*)h->dFilt,
+                           (const int*)rec, (const int*)(rec + ctl_off_oy(h)),
+                           (const int*)(rec + ctl_off_f(h)), (const double*)(rec + ctl_off_zf(h)),
+                           h->dRes, (float*)h->dArgV, h->dArgI, X, Y, TH);
+    CK(hipEventRecord(e1, h->stream));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&t, e0, e1));
+    printf("path alone: %.2f us/launch\n", 1e3 * t / reps);
+    rs_pc_destroy(h);
+    return 0;
+}
