@@ -291,58 +291,66 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Row-tiled forms (the fast path for Y <= 128).  A block owns BK layers x BX
-// rows x the whole Y extent; lanes own columns, so the periodic wrap in y is a
-// 3-cell LDS halo copy and no hot loop divides.  Every load a wave needs is
-// issued before the first LDS store (registers), the 7-tap y and x passes of
-// the excitation and the 7x7 path-integration stencil are register-blocked
-// per column (a lane walks the x direction of its column).
+// Row-tiled forms (the fast path for Y <= 128).  A block (512 threads = 8
+// waves) owns BK layers x BX rows x the whole Y extent; lanes own columns, so
+// the periodic wrap in y is a 3-cell LDS halo and no hot loop divides.  The
+// wrapped layer/row index of every halo row is computed once per block (one
+// modulo per thread) into LDS; then every global load of a wave is issued
+// unconditionally (column clamped) before the first use, so each phase costs
+// one memory round trip.  One halo layer per wave for the stencil passes, which
+// are register-blocked per column (a lane walks the x direction).
 // ---------------------------------------------------------------------------
-constexpr int RT_BX = 4, RT_BK = 2;
+constexpr int RT_BX = 4, RT_BK = 2, RT_NT = 512, RT_NW = RT_NT / 64;
+constexpr int RT_NFMAX = 8;  // filter tables up to this size are preloaded whole
 
-// v in [-k*n, (k+1)*n) for small k (halo coordinates) -> [0, n)
-__device__ inline int wrap_small(int v, int n) {
-    while (v < 0) v += n;
-    while (v >= n) v -= n;
-    return v;
+template <int NW>
+__device__ inline double block_sum_w(double v, double* s_red) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t += s_red[i];
+    return t;
 }
 
 template <typename T, int YP>
-__global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T* __restrict__ Q,
-                                                      double* __restrict__ part,
-                                                      unsigned long long* __restrict__ res_slot,
-                                                      int X, int Y, int TH, SepKernel<T> k) {
-    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF;
-    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = (NR + 3) / 4;
+__global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P, T* __restrict__ Q,
+                                                         double* __restrict__ part,
+                                                         unsigned long long* __restrict__ res_slot,
+                                                         int X, int Y, int TH, SepKernel<T> k) {
+    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF, NW = RT_NW;
+    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = NR / NW;
+    static_assert(NR % NW == 0 && HK == NW && BK * BX == NW, "row tile / wave mapping");
     __shared__ T s_in[NR * RW];
     __shared__ T s_e[HK * BX * YP];
     __shared__ T s_i[HK * BX * YP];
-    __shared__ double s_red[NT / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ int s_row[NR];
+    __shared__ double s_red[NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(0, 0);
+    if (tid < NR) {
+        const int kk = tid / HX, a = tid - kk * HX;
+        s_row[tid] = rs::wrapi(k0 - HALF + kk, TH) * X + rs::wrapi(i0 - HALF + a, X);
+    }
+    __syncthreads();
 
     T v[RPW][JC];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-        const int row = wave + 4 * q;
-        const int kk = row / HX, a = row - kk * HX;
-        const int L = wrap_small(k0 - HALF + kk, TH), r = wrap_small(i0 - HALF + a, X);
-        const T* src = P + ((size_t)L * X + r) * Y;
+        const T* src = P + (size_t)s_row[wave + NW * q] * Y;
 #pragma unroll
-        for (int jc = 0; jc < JC; ++jc) {
-            const int c = lane + 64 * jc;
-            v[q][jc] = (row < NR && c < Y) ? src[c] : T(0);
-        }
+        for (int jc = 0; jc < JC; ++jc) v[q][jc] = src[min(lane + 64 * jc, Y - 1)];
     }
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-        const int row = wave + 4 * q;
+        T* dst = s_in + (wave + NW * q) * RW;
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) {
             const int c = lane + 64 * jc;
-            if (row < NR && c < Y) {
-                T* dst = s_in + row * RW;
+            if (c < Y) {
                 dst[HALF + c] = v[q][jc];
                 if (c < HALF) dst[HALF + Y + c] = v[q][jc];
                 if (c >= Y - HALF) dst[c - (Y - HALF)] = v[q][jc];
@@ -352,8 +360,9 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
     __syncthreads();
     PC_STAMP(0, 1);
 
-    // y pass (7 taps along the row) then x pass (7 rows) in registers, per layer
-    for (int kk = wave; kk < HK; kk += 4) {
+    // y pass (7 taps along the row) then x pass (7 rows) in registers; one layer per wave
+    {
+        const int kk = wave;
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) {
             const int j = lane + 64 * jc;
@@ -388,68 +397,91 @@ __global__ __launch_bounds__(NT) void pc_excite_rows(const T* __restrict__ P, T*
     __syncthreads();
     PC_STAMP(0, 2);
 
-    // theta pass + relu(v - inhib) (posecell_network.py:339-340) + partial sum
+    // theta pass + relu(v - inhib) (posecell_network.py:339-340) + partial sum; one row per wave
     double sum = 0.0;
-    for (int row = wave; row < BK * BX; row += 4) {
-        const int kq = row / BX, i = row - kq * BX;
+    {
+        const int kq = wave / BX, i = wave - kq * BX;
         const int gk = k0 + kq, gi = i0 + i;
-        if (gk >= TH || gi >= X) continue;
+        if (gk < TH && gi < X) {
 #pragma unroll
-        for (int jc = 0; jc < JC; ++jc) {
-            const int j = lane + 64 * jc;
-            if (j >= Y) continue;
-            T e = 0, g = 0;
+            for (int jc = 0; jc < JC; ++jc) {
+                const int j = lane + 64 * jc;
+                if (j >= Y) continue;
+                T e = 0, g = 0;
 #pragma unroll
-            for (int t = 0; t < FL; ++t) {
-                e += k.ge[t] * s_e[((kq + t) * BX + i) * YP + j];
-                g += k.gi[t] * s_i[((kq + t) * BX + i) * YP + j];
+                for (int t = 0; t < FL; ++t) {
+                    e += k.ge[t] * s_e[((kq + t) * BX + i) * YP + j];
+                    g += k.gi[t] * s_i[((kq + t) * BX + i) * YP + j];
+                }
+                const T val = (e - g) * k.scale;
+                const T q = (val < k.inhib) ? T(0) : val - k.inhib;
+                Q[((size_t)gk * X + gi) * Y + j] = q;
+                sum += (double)q;
             }
-            const T val = (e - g) * k.scale;
-            const T q = (val < k.inhib) ? T(0) : val - k.inhib;
-            Q[((size_t)gk * X + gi) * Y + j] = q;
-            sum += (double)q;
         }
     }
-    sum = block_sum(sum, s_red);
-    if (threadIdx.x == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    sum = block_sum_w<NW>(sum, s_red);
+    if (tid == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sum;
     PC_STAMP(0, 3);
 }
 
 template <typename T, int YP>
-__global__ __launch_bounds__(NT) void pc_path_rows(
+__global__ __launch_bounds__(RT_NT) void pc_path_rows(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, const int* __restrict__ ctl_ox, const int* __restrict__ ctl_oy,
-    const int* __restrict__ ctl_f, const double* __restrict__ ctl_zf,
-    unsigned long long* __restrict__ res_slot, T* __restrict__ bmax, unsigned* __restrict__ bidx,
-    int X, int Y, int TH) {
-    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF;
-    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = (NR + 3) / 4;
+    const T* __restrict__ filt, int nf, const int* __restrict__ ctl_ox,
+    const int* __restrict__ ctl_oy, const int* __restrict__ ctl_f,
+    const double* __restrict__ ctl_zf, T* __restrict__ bmax, unsigned* __restrict__ bidx, int X,
+    int Y, int TH) {
+    constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF, NW = RT_NW;
+    constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = NR / NW;
+    constexpr int NPP = 4;  // normalisation partials held per thread (npart <= NPP * RT_NT)
+    static_assert(NR % NW == 0 && HK == NW && BK * BX == NW, "row tile / wave mapping");
     __shared__ T s_win[NR * RW];
     __shared__ T s_r[HK * BX * YP];
+    __shared__ T s_ftab[RT_NFMAX * FT];
     __shared__ T s_f[HK * FT];
-    __shared__ int s_ox[HK], s_oy[HK];
+    __shared__ int s_row[NR];
+    __shared__ int s_L[HK], s_ox[HK], s_oy[HK], s_fi[HK];
     __shared__ T s_zf[FL];
-    __shared__ double s_red[NT / 64];
-    __shared__ T s_bv[NT / 64];
-    __shared__ unsigned s_bl[NT / 64];
+    __shared__ double s_red[NW];
+    __shared__ T s_bv[NW];
+    __shared__ unsigned s_bl[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(1, 0);
 
-    double tot = 0.0;
-    for (int i = tid; i < npart; i += NT) tot += part[i];
-    tot = block_sum(tot, s_red);
-    PC_STAMP(1, 1);
+    // issue everything that does not depend on the control: normalisation partials
+    // (reduced only at the end), the filter table, the theta filter
+    double pt[NPP];
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) {
+        const int i = tid + u * RT_NT;
+        pt[u] = i < npart ? part[i] : 0.0;
+    }
+    double pextra = 0.0;  // npart beyond NPP * RT_NT (huge grids)
+    for (int i = tid + NPP * RT_NT; i < npart; i += RT_NT) pextra += part[i];
+    const bool whole_table = nf <= RT_NFMAX;
+    if (whole_table)
+        for (int idx = tid; idx < nf * FT; idx += RT_NT) s_ftab[idx] = filt[idx];
+    if (tid >= 64 && tid < 64 + FL) s_zf[tid - 64] = (T)ctl_zf[tid - 64];
     if (tid < HK) {
-        const int L = wrap_small(k0 - HALF + tid, TH);
+        const int L = rs::wrapi(k0 - HALF + tid, TH);
+        s_L[tid] = L;
         s_ox[tid] = rs::wrapi(ctl_ox[L], X);   // shifts may exceed the grid (vtrans large)
         s_oy[tid] = rs::wrapi(ctl_oy[L], Y);
+        s_fi[tid] = ctl_f[L];
     }
-    if (tid < FL) s_zf[tid] = (T)ctl_zf[tid];
-    for (int idx = tid; idx < HK * FT; idx += NT) {
-        const int kk = idx / FT, tap = idx - kk * FT;
-        s_f[idx] = filt[ctl_f[wrap_small(k0 - HALF + kk, TH)] * FT + tap];
+    __syncthreads();
+    PC_STAMP(1, 1);
+    if (tid < NR) {
+        const int kk = tid / HX, a = tid - kk * HX;
+        s_row[tid] = s_L[kk] * X + rs::wrapi(i0 - HALF + a + s_ox[kk], X);
     }
+    if (!whole_table)
+        for (int idx = tid; idx < HK * FT; idx += RT_NT) {
+            const int kk = idx / FT;
+            s_f[idx] = filt[s_fi[kk] * FT + idx - kk * FT];
+        }
     __syncthreads();
     PC_STAMP(1, 2);
 
@@ -457,29 +489,21 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
     T v[RPW][JC];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-        const int row = wave + 4 * q;
-        const int kk = row < NR ? row / HX : 0, a = row - kk * HX;
-        const int L = wrap_small(k0 - HALF + kk, TH);
-        const int r = wrap_small(i0 - HALF + a + s_ox[kk], X);
-        const T* src = Q + ((size_t)L * X + r) * Y;
+        const T* src = Q + (size_t)s_row[wave + NW * q] * Y;
 #pragma unroll
-        for (int jc = 0; jc < JC; ++jc) {
-            const int c = lane + 64 * jc;
-            v[q][jc] = (row < NR && c < Y) ? src[c] : T(0);
-        }
+        for (int jc = 0; jc < JC; ++jc) v[q][jc] = src[min(lane + 64 * jc, Y - 1)];
     }
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-        const int row = wave + 4 * q;
-        if (row >= NR) continue;
-        const int kk = row / HX;
+        const int row = wave + NW * q;
+        const int oy = s_oy[row / HX];
+        T* dst = s_win + row * RW;
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) {
             const int c = lane + 64 * jc;
             if (c >= Y) continue;
-            int d = c - s_oy[kk];
+            int d = c - oy;
             if (d < 0) d += Y;
-            T* dst = s_win + row * RW;
             dst[HALF + d] = v[q][jc];
             if (d < HALF) dst[HALF + Y + d] = v[q][jc];
             if (d >= Y - HALF) dst[d - (Y - HALF)] = v[q][jc];
@@ -489,10 +513,12 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
     PC_STAMP(1, 3);
 
     // 7x7 per-layer correlation (:273-274), register-blocked over the BX rows, clamp (:300)
-    for (int kk = wave; kk < HK; kk += 4) {
+    {
+        const int kk = wave;
+        const T* fsrc = whole_table ? s_ftab + s_fi[kk] * FT : s_f + kk * FT;
         T f[FT];
 #pragma unroll
-        for (int t = 0; t < FT; ++t) f[t] = s_f[kk * FT + t];
+        for (int t = 0; t < FT; ++t) f[t] = fsrc[t];
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) {
             const int j = lane + 64 * jc;
@@ -518,59 +544,63 @@ __global__ __launch_bounds__(NT) void pc_path_rows(
             for (int i = 0; i < BX; ++i) s_r[(kk * BX + i) * YP + j] = acc[i] > T(0) ? acc[i] : T(0);
         }
     }
-    __syncthreads();
+    // normalisation total (its loads were issued at entry)
+    double tot = pextra;
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) tot += pt[u];
+    tot = block_sum_w<NW>(tot, s_red);  // includes the barrier that publishes s_r
     PC_STAMP(1, 4);
 
     // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319)
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
-    const T tt = (T)tot;
-    for (int row = wave; row < BK * BX; row += 4) {
-        const int kq = row / BX, i = row - kq * BX;
+    {
+        const T tt = (T)tot;
+        const int kq = wave / BX, i = wave - kq * BX;
         const int gk = k0 + kq, gi = i0 + i;
-        if (gk >= TH || gi >= X) continue;
+        if (gk < TH && gi < X) {
 #pragma unroll
-        for (int jc = 0; jc < JC; ++jc) {
-            const int j = lane + 64 * jc;
-            if (j >= Y) continue;
-            T acc = 0;
+            for (int jc = 0; jc < JC; ++jc) {
+                const int j = lane + 64 * jc;
+                if (j >= Y) continue;
+                T acc = 0;
 #pragma unroll
-            for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * s_zf[z];
-            T val = acc > T(0) ? acc : T(0);
-            if (tot != 0.0) val = val / tt;
-            P[((size_t)gk * X + gi) * Y + j] = val;
-            const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
-            if (val > bv || (val == bv && lin < bl)) {
-                bv = val;
-                bl = lin;
+                for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * s_zf[z];
+                T val = acc > T(0) ? acc : T(0);
+                if (tot != 0.0) val = val / tt;
+                P[((size_t)gk * X + gi) * Y + j] = val;
+                const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
+                if (val > bv || (val == bv && lin < bl)) {
+                    bv = val;
+                    bl = lin;
+                }
             }
         }
     }
-    {
+    // block argmax -> one (value, index) partial per block (pc_argmax_steps reduces)
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const T ov = __shfl_xor(bv, off);
-            const unsigned ol = __shfl_xor(bl, off);
-            if (ov > bv || (ov == bv && ol < bl)) {
-                bv = ov;
-                bl = ol;
+    for (int off = 32; off > 0; off >>= 1) {
+        const T ov = __shfl_xor(bv, off);
+        const unsigned ol = __shfl_xor(bl, off);
+        if (ov > bv || (ov == bv && ol < bl)) {
+            bv = ov;
+            bl = ol;
+        }
+    }
+    if (lane == 0) {
+        s_bv[wave] = bv;
+        s_bl[wave] = bl;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NW; ++w)
+            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                bv = s_bv[w];
+                bl = s_bl[w];
             }
-        }
-        if (lane == 0) {
-            s_bv[wave] = bv;
-            s_bl[wave] = bl;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < NT / 64; ++w)
-                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
-                    bv = s_bv[w];
-                    bl = s_bl[w];
-                }
-            const int b = blockIdx.y * gridDim.x + blockIdx.x;
-            bmax[b] = bv;
-            bidx[b] = bl;
-        }
+        const int b = blockIdx.y * gridDim.x + blockIdx.x;
+        bmax[b] = bv;
+        bidx[b] = bl;
     }
     PC_STAMP(1, 5);
 }
@@ -850,23 +880,23 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
     if (h->tiling == 64 || h->tiling == 128) {
         const dim3 g((h->X + RT_BX - 1) / RT_BX, (h->TH + RT_BK - 1) / RT_BK);
         if (h->tiling == 64)
-            hipLaunchKernelGGL((pc_excite_rows<T, 64>), g, dim3(NT), 0, h->stream, P, Q, h->dPart,
-                               slot, h->X, h->Y, h->TH, k);
+            hipLaunchKernelGGL((pc_excite_rows<T, 64>), g, dim3(RT_NT), 0, h->stream, P, Q,
+                               h->dPart, slot, h->X, h->Y, h->TH, k);
         else
-            hipLaunchKernelGGL((pc_excite_rows<T, 128>), g, dim3(NT), 0, h->stream, P, Q, h->dPart,
-                               slot, h->X, h->Y, h->TH, k);
+            hipLaunchKernelGGL((pc_excite_rows<T, 128>), g, dim3(RT_NT), 0, h->stream, P, Q,
+                               h->dPart, slot, h->X, h->Y, h->TH, k);
         RS_HIP(hipGetLastError());
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
         if (excite_only) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         if (h->tiling == 64)
-            hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(NT), 0, h->stream, Q,
-                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                               slot, bmax, bidx, h->X, h->Y, h->TH);
+            hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(RT_NT), 0, h->stream, Q,
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, cox, coy,
+                               cf, czf, bmax, bidx, h->X, h->Y, h->TH);
         else
-            hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(NT), 0, h->stream, Q,
-                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                               slot, bmax, bidx, h->X, h->Y, h->TH);
+            hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(RT_NT), 0, h->stream, Q,
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, cox, coy,
+                               cf, czf, bmax, bidx, h->X, h->Y, h->TH);
     } else {
         const dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX,
                       (h->TH + EX_BK - 1) / EX_BK);

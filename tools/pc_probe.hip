@@ -122,7 +122,7 @@ int main(int argc, char** argv) {
     const unsigned char* rec = h->dCtl;
     CK(hipEventRecord(e0, h->stream));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((pc_excite_rows<float, 64>), g, dim3(256), 0, h->stream,
+        hipLaunchKernelGGL((pc_excite_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
                            (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->kf);
     CK(hipEventRecord(e1, h->stream));
     CK(hipEventSynchronize(e1));
@@ -130,11 +130,12 @@ int main(int argc, char** argv) {
     printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
     CK(hipEventRecord(e0, h->stream));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((pc_path_rows<float, 64>), g, dim3(256), 0, h->stream, (const float*)h->dQ,
-                           (float*)h->dP, h->dPart, h->nPart, (const float*)h->dFilt,
-                           (const int*)rec, (const int*)(rec + ctl_off_oy(h)),
-                           (const int*)(rec + ctl_off_f(h)), (const double*)(rec + ctl_off_zf(h)),
-                           h->dRes, (float*)h->dArgV, h->dArgI, X, Y, TH);
+        hipLaunchKernelGGL((pc_path_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
+                           (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
+                           (const float*)h->dFilt, h->nf, (const int*)rec,
+                           (const int*)(rec + ctl_off_oy(h)), (const int*)(rec + ctl_off_f(h)),
+                           (const double*)(rec + ctl_off_zf(h)), (float*)h->dArgV, h->dArgI, X,
+                           Y, TH);
     CK(hipEventRecord(e1, h->stream));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&t, e0, e1));
