@@ -45,6 +45,33 @@ struct SepKernel {
     T inhib;
 };
 
+// Per-step control of the path-integration kernel: inline by value (one launch
+// carries its step's shifts, filter rows and theta filter; no copy, no extra
+// dependency) when TH <= CTL_INLINE_MAX, else pointers into a device ring.
+constexpr int CTL_INLINE_MAX = 128;
+struct PcCtlArg {
+    const int* ox;      // ring record, or nullptr -> inline arrays
+    const int* oy;
+    const int* f;
+    const double* zf;
+    short iox[CTL_INLINE_MAX];
+    short ioy[CTL_INLINE_MAX];
+    unsigned char ifi[CTL_INLINE_MAX];
+    double izf[FL];
+};
+
+__device__ inline int ctl_ox(const PcCtlArg& c, int L) { return c.ox ? c.ox[L] : (int)c.iox[L]; }
+__device__ inline int ctl_oy(const PcCtlArg& c, int L) { return c.oy ? c.oy[L] : (int)c.ioy[L]; }
+__device__ inline int ctl_fi(const PcCtlArg& c, int L) { return c.f ? c.f[L] : (int)c.ifi[L]; }
+__device__ inline double ctl_zf(const PcCtlArg& c, int z) { return c.zf ? c.zf[z] : c.izf[z]; }
+
+// float32 argmax: one packed key per block, max-reduced into 8 slots (spread so
+// no address sees more than nblocks/8 atomics); the host takes the max of 8.
+constexpr int RES_SLOTS = 8;
+__device__ inline unsigned long long argmax_key(float v, unsigned lin) {
+    return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
+}
+
 // Phase stamps for the diagnostic probe (tools/pc_probe.hip defines PC_STAMPS);
 // compiled out of the library.
 #ifdef PC_STAMPS
@@ -98,6 +125,9 @@ __global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, 
 
     const int tid = threadIdx.x;
     const int j0 = blockIdx.x * BY, i0 = blockIdx.y * BX, k0 = blockIdx.z * BK;
+    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0 && blockIdx.y == 0 &&
+        blockIdx.z == 0)
+        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
 
     for (int idx = tid; idx < HK * HX * HY; idx += NT) {
         const int kk = idx / (HX * HY);
@@ -174,10 +204,8 @@ __global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, 
 template <typename T, int BX, int BY, int BK>
 __global__ __launch_bounds__(NT) void pc_path_kernel(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, const int* __restrict__ ctl_ox, const int* __restrict__ ctl_oy,
-    const int* __restrict__ ctl_f, const double* __restrict__ ctl_zf,
-    unsigned long long* __restrict__ res_slot, T* __restrict__ bmax, unsigned* __restrict__ bidx,
-    int X, int Y, int TH) {
+    const T* __restrict__ filt, PcCtlArg ctl, unsigned long long* __restrict__ res_slot,
+    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH) {
     constexpr int HX = BX + 2 * HALF, HY = BY + 2 * HALF, HK = BK + 2 * HALF;
     __shared__ T s_win[HK * HX * HY];
     __shared__ T s_r[HK * BX * BY];
@@ -198,14 +226,14 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
 
     if (tid < HK) {
         const int L = rs::wrapi(k0 - HALF + tid, TH);
-        s_ox[tid] = ctl_ox[L];
-        s_oy[tid] = ctl_oy[L];
+        s_ox[tid] = ctl_ox(ctl, L);
+        s_oy[tid] = ctl_oy(ctl, L);
     }
-    if (tid < FL) s_zf[tid] = (T)ctl_zf[tid];
+    if (tid < FL) s_zf[tid] = (T)ctl_zf(ctl, tid);
     for (int idx = tid; idx < HK * FT; idx += NT) {
         const int kk = idx / FT, tap = idx - kk * FT;
         const int L = rs::wrapi(k0 - HALF + kk, TH);
-        s_f[idx] = filt[ctl_f[L] * FT + tap];
+        s_f[idx] = filt[ctl_fi(ctl, L) * FT + tap];
     }
     __syncthreads();
 
@@ -284,8 +312,12 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
                     bl = s_bl[w];
                 }
             const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-            bmax[b] = bv;
-            bidx[b] = bl;
+            if constexpr (sizeof(T) == 4) {
+                atomicMax(res_slot + (b & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
+            } else {
+                bmax[b] = bv;
+                bidx[b] = bl;
+            }
         }
     }
 }
@@ -331,6 +363,8 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(0, 0);
+    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0 && blockIdx.y == 0)
+        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
     if (tid < NR) {
         const int kk = tid / HX, a = tid - kk * HX;
         s_row[tid] = rs::wrapi(k0 - HALF + kk, TH) * X + rs::wrapi(i0 - HALF + a, X);
@@ -428,10 +462,8 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
 template <typename T, int YP>
 __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, int nf, const int* __restrict__ ctl_ox,
-    const int* __restrict__ ctl_oy, const int* __restrict__ ctl_f,
-    const double* __restrict__ ctl_zf, T* __restrict__ bmax, unsigned* __restrict__ bidx, int X,
-    int Y, int TH) {
+    const T* __restrict__ filt, int nf, PcCtlArg ctl, unsigned long long* __restrict__ res_slot,
+    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH) {
     constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF, NW = RT_NW;
     constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = NR / NW;
     constexpr int NPP = 4;  // normalisation partials held per thread (npart <= NPP * RT_NT)
@@ -463,13 +495,13 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     const bool whole_table = nf <= RT_NFMAX;
     if (whole_table)
         for (int idx = tid; idx < nf * FT; idx += RT_NT) s_ftab[idx] = filt[idx];
-    if (tid >= 64 && tid < 64 + FL) s_zf[tid - 64] = (T)ctl_zf[tid - 64];
+    if (tid >= 64 && tid < 64 + FL) s_zf[tid - 64] = (T)ctl_zf(ctl, tid - 64);
     if (tid < HK) {
         const int L = rs::wrapi(k0 - HALF + tid, TH);
         s_L[tid] = L;
-        s_ox[tid] = rs::wrapi(ctl_ox[L], X);   // shifts may exceed the grid (vtrans large)
-        s_oy[tid] = rs::wrapi(ctl_oy[L], Y);
-        s_fi[tid] = ctl_f[L];
+        s_ox[tid] = rs::wrapi(ctl_ox(ctl, L), X);   // shifts may exceed the grid (vtrans large)
+        s_oy[tid] = rs::wrapi(ctl_oy(ctl, L), Y);
+        s_fi[tid] = ctl_fi(ctl, L);
     }
     __syncthreads();
     PC_STAMP(1, 1);
@@ -599,8 +631,12 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 bl = s_bl[w];
             }
         const int b = blockIdx.y * gridDim.x + blockIdx.x;
-        bmax[b] = bv;
-        bidx[b] = bl;
+        if constexpr (sizeof(T) == 4) {
+            atomicMax(res_slot + (b & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
+        } else {
+            bmax[b] = bv;
+            bidx[b] = bl;
+        }
     }
     PC_STAMP(1, 5);
 }
@@ -671,7 +707,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_steps(const T* __restrict__ bmax
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) res[blockIdx.x] = 0xFFFFFFFFull - s_bl[0];
+    if (threadIdx.x == 0) res[(size_t)blockIdx.x * RES_SLOTS] = 0xFFFFFFFFull - s_bl[0];
 }
 
 // Argmax of the stored state (get_pc_max outside update): per-block partials.
@@ -813,10 +849,13 @@ int pc_grow_steps(rs_pc* h, int n) {
     h->dArgV = nullptr; h->dArgI = nullptr;
     RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
     RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
-    RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * cap));
-    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap, hipHostMallocDefault));
-    RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
-    RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
+    RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
+    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * RES_SLOTS * cap,
+                         hipHostMallocDefault));
+    if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
+        RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
+        RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
+    }
     h->ctlCap = cap;
     h->resCap = cap;
     return RS_OK;
@@ -836,17 +875,26 @@ inline size_t ctl_off_oy(const rs_pc* h) { return sizeof(int32_t) * h->TH; }
 inline size_t ctl_off_f(const rs_pc* h) { return 2 * sizeof(int32_t) * h->TH; }
 inline size_t ctl_off_zf(const rs_pc* h) { return rs::round_up(3 * sizeof(int32_t) * h->TH, 16); }
 
+int pc_check_ctl(const rs_pc* h, int n, const int32_t* ox, const int32_t* oy,
+                 const int32_t* fidx, const double* zf) {
+    RS_CHECK(ox && oy && fidx && zf, RS_ERR_ARG, "null control array");
+    for (size_t e = 0; e < (size_t)n * h->TH; ++e) {
+        const int32_t f = fidx[e];
+        RS_CHECK(f >= 0 && f < h->nf, RS_ERR_ARG,
+                 "step %d layer %d: filter index %d outside the table [0, %d)", (int)(e / h->TH),
+                 (int)(e % h->TH), f, h->nf);
+        if (h->TH <= CTL_INLINE_MAX)
+            RS_CHECK(ox[e] >= -32768 && ox[e] <= 32767 && oy[e] >= -32768 && oy[e] <= 32767,
+                     RS_ERR_ARG, "shift (%d, %d) outside the int16 inline control", ox[e], oy[e]);
+    }
+    return RS_OK;
+}
+
 int pc_pack_ctl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                 const double* zf) {
-    RS_CHECK(ox && oy && fidx && zf, RS_ERR_ARG, "null control array");
     const int TH = h->TH;
     for (int s = 0; s < n; ++s) {
         unsigned char* rec = h->hCtl + (size_t)s * h->ctlStride;
-        for (int k = 0; k < TH; ++k) {
-            const int32_t f = fidx[(size_t)s * TH + k];
-            RS_CHECK(f >= 0 && f < h->nf, RS_ERR_ARG,
-                     "step %d layer %d: filter index %d outside the table [0, %d)", s, k, f, h->nf);
-        }
         std::memcpy(rec, ox + (size_t)s * TH, sizeof(int32_t) * TH);
         std::memcpy(rec + ctl_off_oy(h), oy + (size_t)s * TH, sizeof(int32_t) * TH);
         std::memcpy(rec + ctl_off_f(h), fidx + (size_t)s * TH, sizeof(int32_t) * TH);
@@ -862,19 +910,36 @@ const SepKernel<float>& sep_of<float>(const rs_pc* h) { return h->kf; }
 template <>
 const SepKernel<double>& sep_of<double>(const rs_pc* h) { return h->kd; }
 
+// Control of step s: inline (TH <= CTL_INLINE_MAX) or the device ring record.
+void make_ctl(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+              const double* zf, PcCtlArg* c) {
+    if (h->TH <= CTL_INLINE_MAX) {
+        c->ox = c->oy = c->f = nullptr;
+        c->zf = nullptr;
+        const size_t b = (size_t)s * h->TH;
+        for (int k = 0; k < h->TH; ++k) {
+            c->iox[k] = (short)ox[b + k];
+            c->ioy[k] = (short)oy[b + k];
+            c->ifi[k] = (unsigned char)fidx[b + k];
+        }
+        for (int z = 0; z < FL; ++z) c->izf[z] = zf[(size_t)s * FL + z];
+    } else {
+        const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
+        c->ox = reinterpret_cast<const int*>(rec);
+        c->oy = reinterpret_cast<const int*>(rec + ctl_off_oy(h));
+        c->f = reinterpret_cast<const int*>(rec + ctl_off_f(h));
+        c->zf = reinterpret_cast<const double*>(rec + ctl_off_zf(h));
+    }
+}
+
 template <typename T>
-int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
+int pc_launch_step(rs_pc* h, int s, const PcCtlArg* ctl, int prof_base) {
     const T* P = static_cast<const T*>(h->dP);
     T* Q = static_cast<T*>(h->dQ);
     const SepKernel<T>& k = sep_of<T>(h);
-    unsigned long long* slot = h->dRes + s;
-    const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
-    const int* cox = reinterpret_cast<const int*>(rec);
-    const int* coy = reinterpret_cast<const int*>(rec + ctl_off_oy(h));
-    const int* cf = reinterpret_cast<const int*>(rec + ctl_off_f(h));
-    const double* czf = reinterpret_cast<const double*>(rec + ctl_off_zf(h));
-    T* bmax = static_cast<T*>(h->dArgV) + (size_t)s * h->nPathBlocks;
-    unsigned* bidx = h->dArgI + (size_t)s * h->nPathBlocks;
+    unsigned long long* slot = h->dRes + (size_t)s * RES_SLOTS;
+    T* bmax = h->dArgV ? static_cast<T*>(h->dArgV) + (size_t)s * h->nPathBlocks : nullptr;
+    unsigned* bidx = h->dArgI ? h->dArgI + (size_t)s * h->nPathBlocks : nullptr;
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->tiling == 64 || h->tiling == 128) {
@@ -887,16 +952,16 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
                                h->dPart, slot, h->X, h->Y, h->TH, k);
         RS_HIP(hipGetLastError());
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
-        if (excite_only) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
+        if (!ctl) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         if (h->tiling == 64)
             hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(RT_NT), 0, h->stream, Q,
-                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, cox, coy,
-                               cf, czf, bmax, bidx, h->X, h->Y, h->TH);
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
+                               bmax, bidx, h->X, h->Y, h->TH);
         else
             hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(RT_NT), 0, h->stream, Q,
-                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, cox, coy,
-                               cf, czf, bmax, bidx, h->X, h->Y, h->TH);
+                               static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
+                               bmax, bidx, h->X, h->Y, h->TH);
     } else {
         const dim3 gA((h->Y + EX_BY - 1) / EX_BY, (h->X + EX_BX - 1) / EX_BX,
                       (h->TH + EX_BK - 1) / EX_BK);
@@ -904,17 +969,23 @@ int pc_launch_step(rs_pc* h, int s, bool excite_only, int prof_base) {
                            P, Q, h->dPart, slot, h->X, h->Y, h->TH, k);
         RS_HIP(hipGetLastError());
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
-        if (excite_only) return RS_OK;
+        if (!ctl) return RS_OK;
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         const dim3 gB((h->Y + PI_BY - 1) / PI_BY, (h->X + PI_BX - 1) / PI_BX,
                       (h->TH + PI_BK - 1) / PI_BK);
         hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
-                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, cox, coy, cf, czf,
-                           slot, bmax, bidx, h->X, h->Y, h->TH);
+                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, *ctl, slot, bmax,
+                           bidx, h->X, h->Y, h->TH);
     }
     RS_HIP(hipGetLastError());
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 3], h->stream));
     return RS_OK;
+}
+
+unsigned long long slot_max(const unsigned long long* r) {
+    unsigned long long m = r[0];
+    for (int i = 1; i < RES_SLOTS; ++i) m = r[i] > m ? r[i] : m;
+    return m;
 }
 
 void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out) {
@@ -931,28 +1002,33 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     RS_CHECK(n >= 0, RS_ERR_ARG, "negative step count");
     if (n == 0) return RS_OK;
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
     RS_TRY(pc_grow_steps(h, n));
-    RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
-    RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice, h->stream));
+    const bool inline_ctl = h->TH <= CTL_INLINE_MAX;
+    if (!inline_ctl) {
+        RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
+        RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
+                              h->stream));
+    }
     if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
     RS_HIP(hipEventRecord(h->ev0, h->stream));
+    PcCtlArg ctl;
     for (int s = 0; s < n; ++s) {
         const int pb = h->profiling ? 4 * s : -1;
+        make_ctl(h, s, ox, oy, fidx, zf, &ctl);
         if (h->prec == RS_PREC_F32)
-            RS_TRY(pc_launch_step<float>(h, s, false, pb));
+            RS_TRY(pc_launch_step<float>(h, s, &ctl, pb));
         else
-            RS_TRY(pc_launch_step<double>(h, s, false, pb));
+            RS_TRY(pc_launch_step<double>(h, s, &ctl, pb));
     }
-    if (h->prec == RS_PREC_F32)
-        hipLaunchKernelGGL((pc_argmax_steps<float>), dim3(n), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
-    else
+    if (h->prec == RS_PREC_F64) {
         hipLaunchKernelGGL((pc_argmax_steps<double>), dim3(n), dim3(NT), 0, h->stream,
                            static_cast<const double*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
-    RS_HIP(hipGetLastError());
+        RS_HIP(hipGetLastError());
+    }
     RS_HIP(hipEventRecord(h->ev1, h->stream));
-    RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost,
-                          h->stream));
+    RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long) * RES_SLOTS * n,
+                          hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     if (h->profiling) {
@@ -966,7 +1042,8 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         }
     }
     if (out_xyz)
-        for (int s = 0; s < n; ++s) decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
+        for (int s = 0; s < n; ++s)
+            decode_xyz(h, slot_max(h->hRes + (size_t)s * RES_SLOTS), out_xyz + 3 * (size_t)s);
     return RS_OK;
 }
 
@@ -1139,11 +1216,11 @@ int rs_pc_excite(rs_pc* h) {
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
     if (h->prec == RS_PREC_F32) {
-        RS_TRY(pc_launch_step<float>(h, 0, true, -1));
+        RS_TRY(pc_launch_step<float>(h, 0, nullptr, -1));
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
     } else {
-        RS_TRY(pc_launch_step<double>(h, 0, true, -1));
+        RS_TRY(pc_launch_step<double>(h, 0, nullptr, -1));
         hipLaunchKernelGGL((pc_scale_kernel<double>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
     }

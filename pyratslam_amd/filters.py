@@ -121,12 +121,31 @@ class FilterTable:
 
     def rows_for_keys(self, keys):
         """Table rows for per-layer keys; raises KeyError like posecell_network.py:249."""
-        keys = np.asarray(keys)
-        bad = (keys < LUT_KEYS.start) | (keys >= LUT_KEYS.stop)
-        if bad.any():
-            k = int(keys[np.argmax(bad)])
+        idx = np.asarray(keys) - LUT_KEYS.start
+        if idx.min() < 0 or idx.max() >= len(LUT_KEYS):
+            bad = (idx < 0) | (idx >= len(LUT_KEYS))
+            k = int(idx[np.argmax(bad)]) + LUT_KEYS.start
             raise KeyError((k, k))
-        return self._key_to_row[keys - LUT_KEYS.start]
+        return self._key_to_row[idx]
+
+
+_TRIG = {}
+
+
+def layer_trig(th):
+    """(cos, sin) of each layer's heading (dir - mid) * 2pi/TH (posecell_network.py:257-265).
+
+    They do not depend on the odometry, so they are evaluated once per TH with the
+    same NumPy calls; vtrans * cos(...) then has the reference's exact bits.
+    """
+    t = _TRIG.get(th)
+    if t is None:
+        ang = (np.arange(th) - th // 2) * (2.0 * np.pi / th)
+        t = (np.cos(ang), np.sin(ang))
+        for a in t:
+            a.setflags(write=False)
+        _TRIG[th] = t
+    return t
 
 
 def step_control(vtrans, vrot, th, table):
@@ -138,9 +157,9 @@ def step_control(vtrans, vrot, th, table):
     vrot_scale = 2.0 * np.pi / th
     vt = vtrans / PC_CELL_X_SIZE
     vr = vrot / vrot_scale
-    ang = (np.arange(th) - th // 2) * vrot_scale
-    ex = vt * np.cos(ang)
-    ey = vt * np.sin(ang)
+    cos_a, sin_a = layer_trig(th)
+    ex = vt * cos_a
+    ey = vt * sin_a
     rx = np.around(ex)
     ry = np.around(ey)
     keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)   # int() truncates
@@ -162,9 +181,9 @@ def batch_control(odometry, th, table):
     vrot_scale = 2.0 * np.pi / th
     vt = od[:, 0] / PC_CELL_X_SIZE
     vr = od[:, 1] / vrot_scale
-    ang = (np.arange(th) - th // 2) * vrot_scale
-    ex = vt[:, None] * np.cos(ang)[None, :]
-    ey = vt[:, None] * np.sin(ang)[None, :]
+    cos_a, sin_a = layer_trig(th)
+    ex = vt[:, None] * cos_a[None, :]
+    ey = vt[:, None] * sin_a[None, :]
     rx = np.around(ex)
     ry = np.around(ey)
     keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)

@@ -79,6 +79,12 @@ class PoseCellNetwork:
         _lib.check(self._lib.rs_pc_create(*self.shape, ctypes.byref(params), self.device,
                                           ctypes.byref(h)))
         self._h = h
+        # fast path of update(): raw addresses, preallocated output
+        self._update = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p)(('rs_pc_update', self._lib))
+        self._out3 = np.empty(3, dtype=np.int32)
+        self._out3_addr = self._out3.ctypes.data
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
@@ -159,12 +165,12 @@ class PoseCellNetwork:
                 _lib.check(self._lib.rs_pc_excite(self._h))
                 self._max_valid = False
             raise
-        out = np.empty(3, dtype=np.int32)
+        out = self._out3
         with self._mutex:
-            _lib.check(self._lib.rs_pc_update(
-                self._h, _lib.ptr(ox, ctypes.c_int32), _lib.ptr(oy, ctypes.c_int32),
-                _lib.ptr(rows, ctypes.c_int32), _lib.ptr(np.ascontiguousarray(zf), ctypes.c_double),
-                _lib.ptr(out, ctypes.c_int32)))
+            st = self._update(self._h, ox.ctypes.data, oy.ctypes.data, rows.ctypes.data,
+                              zf.ctypes.data, self._out3_addr)
+            if st:
+                _lib.check(st)
             self.max_pc = (int(out[0]), int(out[1]), int(out[2]))
             self._max_valid = True
         return self.max_pc

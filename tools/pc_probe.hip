@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
     double ms = 0;
     rs_pc_last_ms(h, &ms);
     printf("grid %dx%dx%d  tiling %d  blocks %d  run(%d): %.2f us/step\n", X, Y, TH, h->tiling,
-           h->nPart, n, 1e3 * ms / n, h->nPart);
+           h->nPart, n, 1e3 * ms / n);
     // stamps of the last step
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
@@ -119,7 +119,8 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&t, e0, e1));
     printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
-    const unsigned char* rec = h->dCtl;
+    PcCtlArg ctl;
+    make_ctl(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &ctl);
     CK(hipEventRecord(e0, h->stream));
     for (int i = 0; i < reps; ++i)
         hipLaunchKernelGGL((pc_excite_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
@@ -132,10 +133,8 @@ int main(int argc, char** argv) {
     for (int i = 0; i < reps; ++i)
         hipLaunchKernelGGL((pc_path_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
                            (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
-                           (const float*)h->dFilt, h->nf, (const int*)rec,
-                           (const int*)(rec + ctl_off_oy(h)), (const int*)(rec + ctl_off_f(h)),
-                           (const double*)(rec + ctl_off_zf(h)), (float*)h->dArgV, h->dArgI, X,
-                           Y, TH);
+                           (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
+                           (unsigned*)nullptr, X, Y, TH);
     CK(hipEventRecord(e1, h->stream));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&t, e0, e1));
