@@ -49,21 +49,27 @@ struct SepKernel {
 // carries its step's shifts, filter rows and theta filter; no copy, no extra
 // dependency) when TH <= CTL_INLINE_MAX, else pointers into a device ring.
 constexpr int CTL_INLINE_MAX = 128;
-struct PcCtlArg {
-    const int* ox;      // ring record, or nullptr -> inline arrays
-    const int* oy;
-    const int* f;
-    const double* zf;
+struct PcCtlInline {     // single update(): the launch carries the control (~700 B kernarg)
     short iox[CTL_INLINE_MAX];
     short ioy[CTL_INLINE_MAX];
     unsigned char ifi[CTL_INLINE_MAX];
     double izf[FL];
 };
+struct PcCtlRing {       // batched run(): one record per step, uploaded once per batch
+    const int* ox;
+    const int* oy;
+    const int* f;
+    const double* zf;
+};
 
-__device__ inline int ctl_ox(const PcCtlArg& c, int L) { return c.ox ? c.ox[L] : (int)c.iox[L]; }
-__device__ inline int ctl_oy(const PcCtlArg& c, int L) { return c.oy ? c.oy[L] : (int)c.ioy[L]; }
-__device__ inline int ctl_fi(const PcCtlArg& c, int L) { return c.f ? c.f[L] : (int)c.ifi[L]; }
-__device__ inline double ctl_zf(const PcCtlArg& c, int z) { return c.zf ? c.zf[z] : c.izf[z]; }
+__device__ inline int ctl_ox(const PcCtlInline& c, int L) { return c.iox[L]; }
+__device__ inline int ctl_oy(const PcCtlInline& c, int L) { return c.ioy[L]; }
+__device__ inline int ctl_fi(const PcCtlInline& c, int L) { return c.ifi[L]; }
+__device__ inline double ctl_zf(const PcCtlInline& c, int z) { return c.izf[z]; }
+__device__ inline int ctl_ox(const PcCtlRing& c, int L) { return c.ox[L]; }
+__device__ inline int ctl_oy(const PcCtlRing& c, int L) { return c.oy[L]; }
+__device__ inline int ctl_fi(const PcCtlRing& c, int L) { return c.f[L]; }
+__device__ inline double ctl_zf(const PcCtlRing& c, int z) { return c.zf[z]; }
 
 // float32 argmax: one packed key per block, max-reduced into 8 slots (spread so
 // no address sees more than nblocks/8 atomics); the host takes the max of 8.
@@ -201,10 +207,10 @@ __global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, 
 // Kernel 2: path integration (posecell_network.py:252-314) + normalisation
 // (:343-345, applied at the end) + argmax (:317-319)
 // ---------------------------------------------------------------------------
-template <typename T, int BX, int BY, int BK>
+template <typename T, int BX, int BY, int BK, typename CTL>
 __global__ __launch_bounds__(NT) void pc_path_kernel(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, PcCtlArg ctl, unsigned long long* __restrict__ res_slot,
+    const T* __restrict__ filt, CTL ctl, unsigned long long* __restrict__ res_slot,
     T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH) {
     constexpr int HX = BX + 2 * HALF, HY = BY + 2 * HALF, HK = BK + 2 * HALF;
     __shared__ T s_win[HK * HX * HY];
@@ -459,10 +465,10 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
     PC_STAMP(0, 3);
 }
 
-template <typename T, int YP>
+template <typename T, int YP, typename CTL>
 __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, int nf, PcCtlArg ctl, unsigned long long* __restrict__ res_slot,
+    const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
     T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH) {
     constexpr int BX = RT_BX, BK = RT_BK, HX = BX + 2 * HALF, HK = BK + 2 * HALF, NW = RT_NW;
     constexpr int RW = YP + 2 * HALF, JC = YP / 64, NR = HK * HX, RPW = NR / NW;
@@ -910,30 +916,29 @@ const SepKernel<float>& sep_of<float>(const rs_pc* h) { return h->kf; }
 template <>
 const SepKernel<double>& sep_of<double>(const rs_pc* h) { return h->kd; }
 
-// Control of step s: inline (TH <= CTL_INLINE_MAX) or the device ring record.
-void make_ctl(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
-              const double* zf, PcCtlArg* c) {
-    if (h->TH <= CTL_INLINE_MAX) {
-        c->ox = c->oy = c->f = nullptr;
-        c->zf = nullptr;
-        const size_t b = (size_t)s * h->TH;
-        for (int k = 0; k < h->TH; ++k) {
-            c->iox[k] = (short)ox[b + k];
-            c->ioy[k] = (short)oy[b + k];
-            c->ifi[k] = (unsigned char)fidx[b + k];
-        }
-        for (int z = 0; z < FL; ++z) c->izf[z] = zf[(size_t)s * FL + z];
-    } else {
-        const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
-        c->ox = reinterpret_cast<const int*>(rec);
-        c->oy = reinterpret_cast<const int*>(rec + ctl_off_oy(h));
-        c->f = reinterpret_cast<const int*>(rec + ctl_off_f(h));
-        c->zf = reinterpret_cast<const double*>(rec + ctl_off_zf(h));
+// Control of step s as a kernel argument (TH <= CTL_INLINE_MAX) ...
+void make_ctl_inline(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy,
+                     const int32_t* fidx, const double* zf, PcCtlInline* c) {
+    const size_t b = (size_t)s * h->TH;
+    for (int k = 0; k < h->TH; ++k) {
+        c->iox[k] = (short)ox[b + k];
+        c->ioy[k] = (short)oy[b + k];
+        c->ifi[k] = (unsigned char)fidx[b + k];
     }
+    for (int z = 0; z < FL; ++z) c->izf[z] = zf[(size_t)s * FL + z];
 }
 
-template <typename T>
-int pc_launch_step(rs_pc* h, int s, const PcCtlArg* ctl, int prof_base) {
+// ... or as pointers into the device ring record of step s.
+PcCtlRing make_ctl_ring(const rs_pc* h, int s) {
+    const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
+    return PcCtlRing{reinterpret_cast<const int*>(rec),
+                     reinterpret_cast<const int*>(rec + ctl_off_oy(h)),
+                     reinterpret_cast<const int*>(rec + ctl_off_f(h)),
+                     reinterpret_cast<const double*>(rec + ctl_off_zf(h))};
+}
+
+template <typename T, typename CTL>
+int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     const T* P = static_cast<const T*>(h->dP);
     T* Q = static_cast<T*>(h->dQ);
     const SepKernel<T>& k = sep_of<T>(h);
@@ -955,11 +960,11 @@ int pc_launch_step(rs_pc* h, int s, const PcCtlArg* ctl, int prof_base) {
         if (!ctl) return RS_OK;  // rs_pc_excite() normalises with pc_scale_kernel
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         if (h->tiling == 64)
-            hipLaunchKernelGGL((pc_path_rows<T, 64>), g, dim3(RT_NT), 0, h->stream, Q,
+            hipLaunchKernelGGL((pc_path_rows<T, 64, CTL>), g, dim3(RT_NT), 0, h->stream, Q,
                                static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
                                bmax, bidx, h->X, h->Y, h->TH);
         else
-            hipLaunchKernelGGL((pc_path_rows<T, 128>), g, dim3(RT_NT), 0, h->stream, Q,
+            hipLaunchKernelGGL((pc_path_rows<T, 128, CTL>), g, dim3(RT_NT), 0, h->stream, Q,
                                static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
                                bmax, bidx, h->X, h->Y, h->TH);
     } else {
@@ -973,7 +978,7 @@ int pc_launch_step(rs_pc* h, int s, const PcCtlArg* ctl, int prof_base) {
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         const dim3 gB((h->Y + PI_BY - 1) / PI_BY, (h->X + PI_BX - 1) / PI_BX,
                       (h->TH + PI_BK - 1) / PI_BK);
-        hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK>), gB, dim3(NT), 0, h->stream, Q,
+        hipLaunchKernelGGL((pc_path_kernel<T, PI_BX, PI_BY, PI_BK, CTL>), gB, dim3(NT), 0, h->stream, Q,
                            static_cast<T*>(h->dP), h->dPart, h->nPart, filt, *ctl, slot, bmax,
                            bidx, h->X, h->Y, h->TH);
     }
@@ -1004,7 +1009,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
     RS_TRY(pc_grow_steps(h, n));
-    const bool inline_ctl = h->TH <= CTL_INLINE_MAX;
+    const bool inline_ctl = n == 1 && h->TH <= CTL_INLINE_MAX;
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
@@ -1012,14 +1017,22 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     }
     if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
     RS_HIP(hipEventRecord(h->ev0, h->stream));
-    PcCtlArg ctl;
     for (int s = 0; s < n; ++s) {
         const int pb = h->profiling ? 4 * s : -1;
-        make_ctl(h, s, ox, oy, fidx, zf, &ctl);
-        if (h->prec == RS_PREC_F32)
-            RS_TRY(pc_launch_step<float>(h, s, &ctl, pb));
-        else
-            RS_TRY(pc_launch_step<double>(h, s, &ctl, pb));
+        if (inline_ctl) {
+            PcCtlInline c;
+            make_ctl_inline(h, s, ox, oy, fidx, zf, &c);
+            if (h->prec == RS_PREC_F32)
+                RS_TRY((pc_launch_step<float, PcCtlInline>(h, s, &c, pb)));
+            else
+                RS_TRY((pc_launch_step<double, PcCtlInline>(h, s, &c, pb)));
+        } else {
+            const PcCtlRing c = make_ctl_ring(h, s);
+            if (h->prec == RS_PREC_F32)
+                RS_TRY((pc_launch_step<float, PcCtlRing>(h, s, &c, pb)));
+            else
+                RS_TRY((pc_launch_step<double, PcCtlRing>(h, s, &c, pb)));
+        }
     }
     if (h->prec == RS_PREC_F64) {
         hipLaunchKernelGGL((pc_argmax_steps<double>), dim3(n), dim3(NT), 0, h->stream,
@@ -1216,11 +1229,11 @@ int rs_pc_excite(rs_pc* h) {
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
     if (h->prec == RS_PREC_F32) {
-        RS_TRY(pc_launch_step<float>(h, 0, nullptr, -1));
+        RS_TRY((pc_launch_step<float, PcCtlRing>(h, 0, nullptr, -1)));
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
     } else {
-        RS_TRY(pc_launch_step<double>(h, 0, nullptr, -1));
+        RS_TRY((pc_launch_step<double, PcCtlRing>(h, 0, nullptr, -1)));
         hipLaunchKernelGGL((pc_scale_kernel<double>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
     }

@@ -119,8 +119,7 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&t, e0, e1));
     printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
-    PcCtlArg ctl;
-    make_ctl(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &ctl);
+    const PcCtlRing ctl = make_ctl_ring(h, 0);
     CK(hipEventRecord(e0, h->stream));
     for (int i = 0; i < reps; ++i)
         hipLaunchKernelGGL((pc_excite_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
@@ -131,7 +130,7 @@ int main(int argc, char** argv) {
     printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
     CK(hipEventRecord(e0, h->stream));
     for (int i = 0; i < reps; ++i)
-        hipLaunchKernelGGL((pc_path_rows<float, 64>), g, dim3(RT_NT), 0, h->stream,
+        hipLaunchKernelGGL((pc_path_rows<float, 64, PcCtlRing>), g, dim3(RT_NT), 0, h->stream,
                            (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
                            (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
                            (unsigned*)nullptr, X, Y, TH);
