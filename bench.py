@@ -49,7 +49,7 @@ def parse():
     ap.add_argument('--pc-steps', type=int, default=2000, help='timed pose-cell steps')
     ap.add_argument('--pc-warmup', type=int, default=200)
     ap.add_argument('--pc-calls', type=int, default=1000, help='timed per-call update()s')
-    ap.add_argument('--cpu-seconds', type=float, default=8.0, help='CPU baseline budget per leg')
+    ap.add_argument('--cpu-seconds', type=float, default=6.0, help='CPU baseline budget per leg')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
     return ap.parse_args()
@@ -242,36 +242,57 @@ def bench_posecells(args, d):
 
 
 def cpu_baseline(args):
-    """Oracle (NumPy restatement of the reference) on this host, bounded sample."""
+    """The oracle on this host, bounded samples: the C/OpenMP restatement on all
+    OpenMP threads (the reported baseline) and the NumPy restatement (1 thread)."""
+    from oracle import c_oracle as C
     from oracle import posecell as P
     from oracle import view_templates as V
     from pyratslam_amd import synthetic
     T = args.templates_per_gpu
     lib = synthetic.library(T, seed=1)
-    qs, _ = synthetic.queries(lib, 256, seed=2)
+    qs, _ = synthetic.queries(lib, 4096, seed=2)
+    budget = args.cpu_seconds
+    # C / OpenMP: template compares
     n = 0
     t0 = time.perf_counter()
-    while n < len(qs) and time.perf_counter() - t0 < args.cpu_seconds:
+    while n < len(qs) and time.perf_counter() - t0 < budget:
+        C.vt_best(lib, qs[n:n + 16])
+        n += 16
+    dt = time.perf_counter() - t0
+    threads = C.threads()
+    vt = {'value': T * n / dt, 'unit': 'compares/s', 'cores': threads, 'kind': 'port',
+          'sample': '%d queries x %d stored 64x32 u8 templates, oracle/c (C restatement of '
+                    'view_templates.py, OpenMP %d threads)' % (n, T, threads)}
+    # NumPy, single thread
+    n = 0
+    t0 = time.perf_counter()
+    while n < len(qs) and time.perf_counter() - t0 < budget / 2:
         V.vt_scores_library(lib, qs[n])
         n += 1
     dt = time.perf_counter() - t0
-    vt = {'value': T * n / dt, 'unit': 'compares/s', 'cores': 1, 'kind': 'port',
-          'sample': '%d queries x %d stored 64x32 u8 templates, oracle/view_templates.py '
-                    '(NumPy, single thread)' % (n, T)}
+    vt_np = {'value': T * n / dt, 'unit': 'compares/s', 'cores': 1, 'kind': 'port',
+             'sample': '%d queries, oracle/view_templates.py (NumPy)' % n}
     shape = tuple(int(s) for s in args.pc_shape.split(','))
-    net = P.PoseCellOracle(shape)
-    net.inject(1, tuple(s // 2 for s in shape))
-    od = synthetic.odometry(1000, seed=0)
-    k = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
-        net.update(od[k])
-        k += 1
-    dt = time.perf_counter() - t0
-    pc = {'value': k / dt, 'unit': 'steps/s', 'cores': 1, 'kind': 'port',
-          'sample': '%d updates of a %s grid, oracle/posecell.py (NumPy float64, 343-tap '
-                    'direct correlation like the reference kernel, single thread)' % (k, shape)}
-    return vt, pc
+    od = synthetic.odometry(100000, seed=0)
+    res = {}
+    for name, cls, share in (('c', C.PoseCellC, 1.0), ('numpy', P.PoseCellOracle, 0.5)):
+        net = cls(shape)
+        net.inject(1, tuple(s // 2 for s in shape))
+        k = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget * share:
+            net.update(od[k])
+            k += 1
+        res[name] = (k, time.perf_counter() - t0)
+    k, dt = res['c']
+    pc = {'value': k / dt, 'unit': 'steps/s', 'cores': threads, 'kind': 'port',
+          'sample': '%d updates of a %s grid, oracle/c (C restatement of the three OpenCL '
+                    'kernels in float64, 343-tap direct correlation, OpenMP %d threads; host '
+                    'control in NumPy)' % (k, shape, threads)}
+    k, dt = res['numpy']
+    pc_np = {'value': k / dt, 'unit': 'steps/s', 'cores': 1, 'kind': 'port',
+             'sample': '%d updates, oracle/posecell.py (NumPy float64)' % k}
+    return vt, vt_np, pc, pc_np
 
 
 def main():
@@ -329,9 +350,11 @@ def main():
                           'known_answer_hits_correct': tv['hits_correct']},
     }
     if d.world == 1 and not args.no_cpu_baseline:
-        vt_cpu, pc_cpu = cpu_baseline(args)
+        vt_cpu, vt_np, pc_cpu, pc_np = cpu_baseline(args)
         out['cpu_baseline'] = vt_cpu
+        out['cpu_baseline_numpy'] = vt_np
         out['pose_cell']['cpu_baseline'] = pc_cpu
+        out['pose_cell']['cpu_baseline_numpy'] = pc_np
     print(json.dumps(out), flush=True)
     d.close()
 

@@ -138,8 +138,14 @@ __global__ __launch_bounds__(64) void vt_scan_lane_kernel(const uint4* __restric
                                                           const uint2* __restrict__ qf, int nq,
                                                           ScanOut out, int rank, int nranks) {
     constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
-    const int tb = blockIdx.x % ntb;
-    const int qbase = (blockIdx.x / ntb) * NQ;
+    // XCD-aware mapping (speed only): blocks b and b+8 are dealt to the same XCD, so
+    // XCD x takes query groups qg = x (mod 8) against the whole library -- its L2
+    // holds the library plus 1/8 of the query forms.
+    const int j = blockIdx.x >> 3;
+    const int tb = j % ntb;
+    const int qg = (j / ntb) * 8 + (blockIdx.x & 7);
+    if (qg * NQ >= nq) return;
+    const int qbase = qg * NQ;
     const int lane = threadIdx.x;
     uint32_t acc[NQ][NO];
 #pragma unroll
@@ -269,8 +275,14 @@ __global__ __launch_bounds__(64) void vt_scan_carry_kernel(const uint4* __restri
                                                            int nq, ScanOut out, int rank,
                                                            int nranks) {
     constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1, R0 = M, R1 = H - M;
-    const int tb = blockIdx.x % ntb;
-    const int qbase = (blockIdx.x / ntb) * NQ;
+    // XCD-aware mapping (speed only): blocks b and b+8 are dealt to the same XCD, so
+    // XCD x takes query groups qg = x (mod 8) against the whole library -- its L2
+    // holds the library plus 1/8 of the query forms.
+    const int j = blockIdx.x >> 3;
+    const int tb = j % ntb;
+    const int qg = (j / ntb) * 8 + (blockIdx.x & 7);
+    if (qg * NQ >= nq) return;
+    const int qbase = qg * NQ;
     const int lane = threadIdx.x;
     uint32_t cnt[NQ][NO];
     uint32_t A[NO];
@@ -625,7 +637,7 @@ int vt_launch_scan(rs_vt* h, const uint4* lib, int64_t count, int nq, ScanOut ou
     } else if (fast) {
         constexpr int NQ = 2;
         const int nqg = (nq + NQ - 1) / NQ;
-        const dim3 grid((unsigned)(ntb * nqg));
+        const dim3 grid((unsigned)(ntb * ((nqg + 7) / 8) * 8));
         if (h->carry) {
             if (h->H == 64)
                 hipLaunchKernelGGL((vt_scan_carry_kernel<64, NQ, MATRIX>), grid, dim3(64), 0,

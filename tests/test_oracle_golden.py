@@ -91,3 +91,21 @@ def test_vt_trace_bit_exact(name):
     assert np.array_equal(idx, d['index'])
     assert np.array_equal(np.stack(o.templates), d['templates'])
     assert np.array_equal(np.array(o.locations), d['locations'])
+
+
+def test_c_oracle_matches_reference():
+    """The C/OpenMP restatement (oracle/c) is a second checker and the CPU baseline."""
+    from oracle import c_oracle as C
+    for name in ('pc32_s1', 'pc_ragged', 'pc_simulate'):
+        case = load_golden(name)
+        net = C.PoseCellC(tuple(case['shape']))
+        net.inject(1, tuple(case['inject']))
+        for s, v in enumerate(case['odom']):
+            assert net.update(v) == tuple(case['max_pc'][s])
+            assert np.abs(net.posecells - dense_state(case, s)).max() < 1e-12
+    lib = V.synthetic_library(300, seed=3)
+    qs, _ = V.synthetic_queries(lib, 40, seed=4)
+    sc, ix = C.vt_best(lib, qs)
+    for i, q in enumerate(qs):
+        ref = V.vt_scores_library(lib, q)
+        assert sc[i] == ref.min() and ix[i] == np.argmin(ref)
