@@ -190,6 +190,76 @@ __global__ __launch_bounds__(64) void vt_scan_lane_kernel(const uint4* __restric
     }
 }
 
+// --- row-blocked throughput form: the query rows [M, H-M) of a column are split
+// into RB blocks; a block hoists only the template rows its 2M-1 offsets touch
+// (RS + 2M - 2 rows instead of H), which keeps the kernel near 128 VGPRs (4 waves
+// per SIMD) at the cost of re-reading the overlapping quads (L1 hits).
+template <int H, int NQ, int RB, int B>
+__device__ inline void scan_block(const uint4* __restrict__ col, const uint2* __restrict__ qf,
+                                  int WD, int c, int qbase, int nq, uint32_t (&acc)[NQ][2 * FAST_M - 1]) {
+    constexpr int M = FAST_M, NO = 2 * M - 1, R0 = M, R1 = H - M;
+    constexpr int RS = (R1 - R0 + RB - 1) / RB;
+    constexpr int r_lo = R0 + B * RS;
+    constexpr int r_hi = (r_lo + RS < R1) ? r_lo + RS : R1;
+    constexpr int s_lo = r_lo - (M - 1), s_hi = r_hi - 1 + (M - 1);
+    constexpr int q_lo = s_lo / 4, q_hi = s_hi / 4, NQD = q_hi - q_lo + 1;
+    uint32_t aL[4 * NQD], aH[4 * NQD];
+#pragma unroll
+    for (int q = 0; q < NQD; ++q) {
+        const uint4 v = col[(size_t)(q_lo + q) * 64];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
+            aH[4 * q + k] = w[k] & 0x80808080u;
+        }
+    }
+#pragma unroll
+    for (int r = r_lo; r < r_hi; ++r) {
+#pragma unroll
+        for (int n = 0; n < NQ; ++n) {
+            const int qi = min(qbase + n, nq - 1);
+            const uint2 f = qf[((size_t)qi * WD + c) * H + r];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) {
+                const int sidx = r + o - (M - 1) - 4 * q_lo;
+                acc[n][o] = wrapped_pair(aL[sidx], aH[sidx], f, acc[n][o]);
+            }
+        }
+    }
+    if constexpr (B + 1 < RB) scan_block<H, NQ, RB, B + 1>(col, qf, WD, c, qbase, nq, acc);
+}
+
+template <int H, int NQ, int RB, bool MATRIX>
+__global__ __launch_bounds__(64) void vt_scan_rb_kernel(const uint4* __restrict__ lib, int ntb,
+                                                        int64_t count, int WD,
+                                                        const uint2* __restrict__ qf, int nq,
+                                                        ScanOut out, int rank, int nranks) {
+    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
+    const int j = blockIdx.x >> 3;
+    const int tb = j % ntb;
+    const int qg = (j / ntb) * 8 + (blockIdx.x & 7);
+    if (qg * NQ >= nq) return;
+    const int qbase = qg * NQ;
+    const int lane = threadIdx.x;
+    uint32_t acc[NQ][NO];
+#pragma unroll
+    for (int n = 0; n < NQ; ++n)
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
+    for (int c = 0; c < WD; ++c)
+        scan_block<H, NQ, RB, 0>(lib + ((size_t)(tb * WD + c) * HQ) * 64 + lane, qf, WD, c, qbase,
+                                 nq, acc);
+    const int64_t slot = (int64_t)tb * 64 + lane;
+#pragma unroll
+    for (int n = 0; n < NQ; ++n) {
+        uint32_t sc = acc[n][0];
+#pragma unroll
+        for (int o = 1; o < NO; ++o) sc = min(sc, acc[n][o]);
+        emit_score<MATRIX>(out, slot, count, qbase + n, nq, sc, rank, nranks, lane == 0);
+    }
+}
+
 // --- latency form: 8 lanes per template (one dword column each), 8 templates
 // per wave; the per-offset sums are combined across the 8 column lanes.
 template <int H, int NQ>
@@ -488,6 +558,7 @@ struct rs_vt {
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
     bool carry = true;  // carry-count scan (default) or v_sad_u8 scan (RS_VT_SCAN=sad)
+    int scan_rb = 0;    // row-blocked v_sad_u8 scan with this many row blocks (RS_VT_SCAN=rb2|rb3)
 };
 
 namespace {
@@ -638,7 +709,16 @@ int vt_launch_scan(rs_vt* h, const uint4* lib, int64_t count, int nq, ScanOut ou
         constexpr int NQ = 2;
         const int nqg = (nq + NQ - 1) / NQ;
         const dim3 grid((unsigned)(ntb * ((nqg + 7) / 8) * 8));
-        if (h->carry) {
+        if (h->scan_rb == 2 && h->H == 64) {
+            hipLaunchKernelGGL((vt_scan_rb_kernel<64, NQ, 2, MATRIX>), grid, dim3(64), 0,
+                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+        } else if (h->scan_rb == 3 && h->H == 64) {
+            hipLaunchKernelGGL((vt_scan_rb_kernel<64, NQ, 3, MATRIX>), grid, dim3(64), 0,
+                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+        } else if (h->scan_rb == 2 && h->H == 32) {
+            hipLaunchKernelGGL((vt_scan_rb_kernel<32, NQ, 2, MATRIX>), grid, dim3(64), 0,
+                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
+        } else if (h->carry) {
             if (h->H == 64)
                 hipLaunchKernelGGL((vt_scan_carry_kernel<64, NQ, MATRIX>), grid, dim3(64), 0,
                                    h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
@@ -822,7 +902,11 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
     h->H = H; h->W = W; h->M = max_offset; h->thr = thr; h->device = device;
     h->WD = (W + 3) / 4;
     h->HQ = (H + 3) / 4;
-    if (const char* e = std::getenv("RS_VT_SCAN")) h->carry = std::strcmp(e, "sad") != 0;
+    if (const char* e = std::getenv("RS_VT_SCAN")) {
+        h->carry = std::strcmp(e, "carry") == 0;
+        if (std::strcmp(e, "rb2") == 0) h->scan_rb = 2;
+        if (std::strcmp(e, "rb3") == 0) h->scan_rb = 3;
+    }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
