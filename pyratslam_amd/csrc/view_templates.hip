@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -519,6 +520,272 @@ __global__ __launch_bounds__(64) void vt_scan_generic_kernel(const uint4* __rest
     emit_score<MATRIX>(out, (int64_t)tb * 64 + lane, count, qi, nq, best, rank, nranks, lane == 0);
 }
 
+// ===========================================================================
+// Bit-plane scan (default for W = 32, H in {32, 64}, max_offset 8).
+//
+// (T - Q) mod 256 = T - Q + 256 [T < Q], so a score is
+//   score(o) = TS(o) - QS + 256 * B(o),
+// TS(o) = the template's byte sum over rows [M+o, H-M+o) (stored with the
+// template), QS = the query's byte sum over rows [M, H-M), and B(o) = the number
+// of byte pairs with T < Q.  B is counted bit-sliced: a unit of 4 rows x 8
+// columns (32 bytes) is stored as 8 bit planes (plane k, bit i = bit k of byte
+// i), and [T < Q] for all 32 pairs of a unit is the borrow out of T - Q,
+//   b = maj(~T_k, Q_k, b)  for k = 0..7   (one v_bitop3_b32 each, table 0x8E),
+// followed by one v_bcnt_u32_b32 into the offset's counter: 9 VALU per
+// 32 byte pairs, against 3 per 4 pairs for the byte-SWAR forms above.
+//
+// Template planes: uint4 chunk ((((tb*CG + cg)*NU + j)*2 + g)*64 + t) holds
+// planes 4g..4g+3 of unit j (rows 4j..4j+3, columns 8cg..8cg+7) of slot
+// tb*64 + t.  TS: tsum[(tb*16 + o+M-1)*64 + t].
+// Query planes: for every start row s in [M-3, H-M-1] and column group cg, the
+// unit of rows s..s+3 with rows outside [M, H-M) zeroed (a zero byte never
+// borrows), qp[((q*CG + cg)*NS + s-(M-3))*8 + k]; qsum[q] = QS (raw bytes).
+//
+// A block is CG waves (one per column group) x 64 templates.  Wave cg keeps
+// its NU units x 8 planes in VGPRs and streams query planes through SGPRs
+// (wave-uniform scalar loads).  Template unit j meets query unit s at offset
+// o = 4j - s.  The CG partial counts per (query, offset, template) meet in LDS.
+// ===========================================================================
+constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
+
+// Per-wave start/end stamps for the diagnostic probe (tools/vt_probe.hip defines
+// VT_STAMPS and the vt_dbg buffer): realtime (100 MHz), shader clock, hw ids.
+#ifdef VT_STAMPS
+#define VT_STAMP(slot)                                                                     \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0) {                                                     \
+            unsigned hw_, xcc_;                                                            \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
+            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * PL_CG + (threadIdx.x >> 6)) * 6; \
+            d_[(slot) * 3 + 0] = __builtin_amdgcn_s_memrealtime();                         \
+            d_[(slot) * 3 + 1] = __builtin_amdgcn_s_memtime();                             \
+            d_[(slot) * 3 + 2] = ((unsigned long long)xcc_ << 32) | hw_;                   \
+        }                                                                                  \
+    } while (0)
+#else
+#define VT_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+constexpr int PL_NB = PL_CG;   // queries per LDS reduction batch (one per wave)
+
+__device__ inline uint32_t plane_borrows(const uint32_t (&t)[8], const uint32_t* q) {
+    uint32_t b = __builtin_amdgcn_bitop3_b32(t[0], q[0], 0u, 0x8E);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) b = __builtin_amdgcn_bitop3_b32(t[k], q[k], b, 0x8E);
+    return b;
+}
+
+// One block per stored template: planes + TS of raw template src[t] into slot dst[t].
+__global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __restrict__ raw,
+                                                             const int32_t* __restrict__ src,
+                                                             const int64_t* __restrict__ dst,
+                                                             int H, int M,
+                                                             uint32_t* __restrict__ planes,
+                                                             uint32_t* __restrict__ tsum) {
+    constexpr int W = 8 * PL_CG;
+    __shared__ uint32_t s_row[256];
+    const uint8_t* T = raw + (size_t)src[blockIdx.x] * H * W;
+    const int64_t slot = dst[blockIdx.x];
+    const int64_t tb = slot >> 6, tl = slot & 63;
+    const int NU = H / 4, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31;
+    for (int u0 = 2 * wave; u0 < PL_CG * NU; u0 += 8) {
+        const int u = u0 + (lane >> 5);
+        const int cg = u / NU, j = u - cg * NU;
+        const uint32_t byte = u < PL_CG * NU ? T[(size_t)(4 * j + (i >> 3)) * W + 8 * cg + (i & 7)] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const unsigned long long m = __ballot((byte >> k) & 1u);
+            if (i == k && u < PL_CG * NU)
+                planes[((((tb * PL_CG + cg) * NU + j) * 2 + (k >> 2)) * 64 + tl) * 4 + (k & 3)] =
+                    (uint32_t)(lane < 32 ? m : m >> 32);
+        }
+    }
+    for (int r = threadIdx.x; r < H; r += blockDim.x) {
+        uint32_t acc = 0;
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(T + (size_t)r * W);
+#pragma unroll
+        for (int d = 0; d < W / 4; ++d) acc = __builtin_amdgcn_sad_u8(row[d], 0u, acc);
+        s_row[r] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        const int o = (int)threadIdx.x - (M - 1);
+        uint32_t ts = 0;
+        if (threadIdx.x < 2 * M - 1)
+            for (int r = M + o; r < H - M + o; ++r) ts += s_row[r];
+        tsum[(tb * 16 + threadIdx.x) * 64 + tl] = ts;
+    }
+}
+
+// One block per query: query planes for every start row, and QS.
+__global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restrict__ raw, int H,
+                                                        int M, uint32_t* __restrict__ qp,
+                                                        uint32_t* __restrict__ qsum) {
+    constexpr int W = 8 * PL_CG;
+    __shared__ uint32_t s_red[4];
+    const int NS = H - 2 * M + 3, S0 = M - 3;
+    const uint8_t* Q = raw + (size_t)blockIdx.x * H * W;
+    uint32_t* out = qp + (size_t)blockIdx.x * PL_CG * NS * 8;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31;
+    for (int u0 = 2 * wave; u0 < PL_CG * NS; u0 += 8) {
+        const int u = u0 + (lane >> 5);
+        const int cg = u / NS, si = u - cg * NS, r = S0 + si + (i >> 3);
+        const uint32_t byte =
+            (u < PL_CG * NS && r >= M && r < H - M) ? Q[(size_t)r * W + 8 * cg + (i & 7)] : 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const unsigned long long m = __ballot((byte >> k) & 1u);
+            if (i == k && u < PL_CG * NS) out[(size_t)u * 8 + k] = (uint32_t)(lane < 32 ? m : m >> 32);
+        }
+    }
+    uint32_t part = 0;
+    const uint32_t* rows = reinterpret_cast<const uint32_t*>(Q + (size_t)M * W);
+    for (int d = threadIdx.x; d < (H - 2 * M) * W / 4; d += blockDim.x)
+        part = __builtin_amdgcn_sad_u8(rows[d], 0u, part);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    if (lane == 0) s_red[wave] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) qsum[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+}
+
+// One query start row S against the template units it meets (o = 4J - S within
+// +-(M-1): 3 or 4 units).  The borrow chains of those units are interleaved
+// plane by plane, so consecutive bitop3s are independent (a single chain would
+// stall on every instruction).  All indices are compile-time.
+template <int H, int S>
+__device__ __forceinline__ void plane_row(const uint32_t (&P)[H / 4][8], const uint32_t* q,
+                                          uint32_t (&acc)[2 * FAST_M - 1]) {
+    constexpr int M = FAST_M, NU = H / 4;
+    constexpr int JA = (S - (M - 1)) > 0 ? (S - (M - 1) + 3) / 4 : 0;  // first J with o >= -(M-1)
+    constexpr int JB0 = (S + (M - 1)) / 4;                             // last J with o <= M-1
+    constexpr int JB = JB0 < NU - 1 ? JB0 : NU - 1;
+    constexpr int NJ = JB - JA + 1;
+    static_assert(NJ >= 1 && NJ <= 4, "units per query row");
+    uint32_t b[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][0], q[0], 0u, 0x8E);
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][k], q[k], b[j], 0x8E);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        // v_bcnt's own accumulator (asm keeps the compiler from re-associating
+        // the counts into half-rate v_add3_u32)
+        uint32_t& a = acc[4 * (JA + j) - S + M - 1];
+        asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(a) : "v"(b[j]), "v"(a));
+    }
+}
+
+// Query planes reach SGPRs in chunks of PL_QC rows, double-buffered: at a
+// chunk boundary wait for the chunk (scalar loads return out of order, so only
+// lgkmcnt(0) is exact), then issue the next chunk's loads, then compute; the
+// scheduling barriers keep the compiler from hoisting the next loads above the
+// wait, which would expose their latency on every row.
+constexpr int PL_QC = 4;
+constexpr unsigned WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched (gfx9)
+
+template <int H, int C>
+__device__ __forceinline__ void plane_load_chunk(const uint32_t* __restrict__ qf,
+                                                 uint32_t (&dst)[PL_QC * 8]) {
+    constexpr int NS = H - 2 * FAST_M + 3;
+#pragma unroll
+    for (int i = 0; i < PL_QC * 8; ++i)
+        if (C * PL_QC * 8 + i < NS * 8) dst[i] = qf[C * PL_QC * 8 + i];
+}
+
+template <int H, int S>
+__device__ __forceinline__ void plane_rows(const uint32_t (&P)[H / 4][8], const uint32_t* qf,
+                                           uint32_t (&qb)[2][PL_QC * 8],
+                                           uint32_t (&acc)[2 * FAST_M - 1]) {
+    constexpr int M = FAST_M, S0 = M - 3, S1 = H - M - 1, NS = S1 - S0 + 1;
+    constexpr int rel = S - S0, ci = rel / PL_QC, r = rel % PL_QC;
+    constexpr int NC = (NS + PL_QC - 1) / PL_QC;
+    if constexpr (r == 0) {
+        __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ci + 1 < NC) plane_load_chunk<H, ci + 1>(qf, qb[(ci + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    plane_row<H, S>(P, &qb[ci & 1][r * 8], acc);
+    if constexpr (S < S1) plane_rows<H, S + 1>(P, qf, qb, acc);
+}
+
+template <int H, bool MATRIX>
+__global__ __launch_bounds__(64 * PL_CG) void vt_scan_plane_kernel(
+    const uint4* __restrict__ planes, const uint32_t* __restrict__ tsum, int ntb, int64_t count,
+    const uint32_t* __restrict__ qp, const uint32_t* __restrict__ qsum, int nq, int nqc,
+    ScanOut out, int rank, int nranks) {
+    constexpr int M = FAST_M, NU = H / 4, NO = 2 * M - 1, S0 = M - 3, S1 = H - M - 1;
+    constexpr int NS = S1 - S0 + 1, NK = (NO + 1) / 2;
+    __shared__ uint32_t s_part[PL_NB][NK][PL_CG][64];  // u16 pairs: offsets 2k, 2k+1
+    __shared__ uint32_t s_ts[16][64];
+    int tb, qk;
+    if (nqc >= 8) {  // XCD-aware: blocks b and b+8 share an XCD (and its L2)
+        const int j = blockIdx.x >> 3;
+        tb = j % ntb;
+        qk = (j / ntb) * 8 + (blockIdx.x & 7);
+    } else {
+        tb = blockIdx.x % ntb;
+        qk = blockIdx.x / ntb;
+    }
+    // chunk qk of nqc near-equal query ranges (sizes differ by at most one)
+    const int q0 = (int)((int64_t)qk * nq / nqc), q1 = (int)((int64_t)(qk + 1) * nq / nqc);
+    if (q0 >= q1) return;  // whole block: before any barrier
+    VT_STAMP(0);
+    const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 16 * 64; i += 64 * PL_CG)
+        s_ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
+    uint32_t P[NU][8];
+    {
+        const uint4* src = planes + (size_t)(tb * PL_CG + cg) * NU * 128 + lane;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const uint4 a = src[(2 * j) * 64], b = src[(2 * j + 1) * 64];
+            P[j][0] = a.x; P[j][1] = a.y; P[j][2] = a.z; P[j][3] = a.w;
+            P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
+        }
+    }
+    const int64_t slot = (int64_t)tb * 64 + lane;
+    for (int qb = q0; qb < q1; qb += PL_NB) {
+        const int nb = min(PL_NB, q1 - qb);
+#pragma unroll 1
+        for (int b = 0; b < nb; ++b) {
+            const int qi = qb + b;
+            const uint32_t* qf = qp + ((size_t)qi * PL_CG + cg) * NS * 8;
+            uint32_t acc[NO];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) acc[o] = 0u;
+            uint32_t qb[2][PL_QC * 8];
+            plane_load_chunk<H, 0>(qf, qb[0]);
+            plane_rows<H, S0>(P, qf, qb, acc);
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                s_part[b][k][cg][lane] = acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u);
+        }
+        __syncthreads();
+        const int qi = qb + cg;  // wave cg finishes query qb + cg of the batch
+        if (qi < q1) {
+            uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                uint32_t t = 0;  // per-half sums stay < 2^16: no carry between the halves
+#pragma unroll
+                for (int c = 0; c < PL_CG; ++c) t += s_part[cg][k][c][lane];
+                best = min(best, s_ts[2 * k][lane] + 256u * (t & 0xFFFFu));
+                if (2 * k + 1 < NO) best = min(best, s_ts[2 * k + 1][lane] + 256u * (t >> 16));
+            }
+            emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
+        }
+        __syncthreads();
+    }
+    VT_STAMP(1);
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -557,13 +824,48 @@ struct rs_vt {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
-    bool carry = true;  // carry-count scan (default) or v_sad_u8 scan (RS_VT_SCAN=sad)
+    bool carry = true;  // carry-count scan or v_sad_u8 scan (RS_VT_SCAN=sad)
     int scan_rb = 0;    // row-blocked v_sad_u8 scan with this many row blocks (RS_VT_SCAN=rb2|rb3)
+    // bit-plane scan (default when W == 32, H in {32, 64}, max_offset 8; RS_VT_SCAN=plane):
+    // planes + TS of the library and candidate slots, query planes + raw sums
+    bool planar = false;
+    uint32_t* dLibP = nullptr;
+    uint32_t* dLibTs = nullptr;
+    uint32_t* dCandP = nullptr;
+    uint32_t* dCandTs = nullptr;
+    uint32_t* dQp = nullptr;
+    uint32_t* dQsumRaw = nullptr;
+    int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
 };
 
 namespace {
 
 size_t tblock_bytes(const rs_vt* h) { return (size_t)h->WD * h->HQ * 64 * 16; }
+size_t pblock_bytes(const rs_vt* h) { return (size_t)PL_CG * (h->H / 4) * 128 * 16; }
+constexpr size_t TS_BLOCK_BYTES = 16 * 64 * sizeof(uint32_t);
+int plane_ns(const rs_vt* h) { return h->H - 2 * h->M + 3; }
+
+// (Re)allocate a slot buffer of `blocks` 64-slot blocks of `bb` bytes, keeping
+// the first `keep` blocks.
+int vt_realloc_blocks(rs_vt* h, void** buf, int64_t keep, int64_t blocks, size_t bb) {
+    void* nb = nullptr;
+    const size_t bytes = (size_t)blocks * bb;
+    hipError_t e = hipMalloc(&nb, bytes);
+    if (e != hipSuccess) {
+        rs::set_error("template buffer growth to %lld slots (%zu bytes) failed: %s",
+                      (long long)blocks * 64, bytes, hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? RS_ERR_NOMEM : RS_ERR_HIP;
+    }
+    RS_HIP(hipMemsetAsync(nb, 0, bytes, h->stream));
+    if (*buf) {
+        if (keep > 0)
+            RS_HIP(hipMemcpyAsync(nb, *buf, (size_t)keep * bb, hipMemcpyDeviceToDevice, h->stream));
+        RS_HIP(hipStreamSynchronize(h->stream));
+        RS_HIP(hipFree(*buf));
+    }
+    *buf = nb;
+    return RS_OK;
+}
 
 int64_t local_count_of(const rs_vt* h, int64_t global_count) {
     if (global_count <= h->rank) return 0;
@@ -591,6 +893,10 @@ int vt_grow_lib(rs_vt* h, int64_t need_slots) {
         RS_HIP(hipFree(h->dLib));
     }
     h->dLib = nl;
+    if (h->planar) {
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dLibP, h->localCap / 64, cap / 64, pblock_bytes(h)));
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dLibTs, h->localCap / 64, cap / 64, TS_BLOCK_BYTES));
+    }
     h->localCap = cap;
     return RS_OK;
 }
@@ -605,7 +911,14 @@ int vt_grow_queries(rs_vt* h, int nq) {
     if (h->dQsum) RS_HIP(hipFree(h->dQsum));
     if (h->dBest) RS_HIP(hipFree(h->dBest));
     if (h->hBest) RS_HIP(hipHostFree(h->hBest));
+    if (h->dQp) RS_HIP(hipFree(h->dQp));
+    if (h->dQsumRaw) RS_HIP(hipFree(h->dQsumRaw));
+    h->dQp = h->dQsumRaw = nullptr;
     const size_t qb = (size_t)h->H * h->W;
+    if (h->planar) {
+        RS_HIP(hipMalloc(&h->dQp, sizeof(uint32_t) * PL_CG * plane_ns(h) * 8 * (size_t)cap));
+        RS_HIP(hipMalloc(&h->dQsumRaw, sizeof(uint32_t) * cap));
+    }
     RS_HIP(hipMalloc(&h->dQraw, qb * cap));
     RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dQf, sizeof(uint2) * (size_t)h->WD * h->H * cap));
@@ -650,6 +963,10 @@ int vt_grow_cand(rs_vt* h, int64_t slots) {
     while (cap < slots) cap *= 2;
     if (h->dCand) RS_HIP(hipFree(h->dCand));
     RS_HIP(hipMalloc(&h->dCand, (size_t)(cap / 64) * tblock_bytes(h)));
+    if (h->planar) {
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dCandP, 0, cap / 64, pblock_bytes(h)));
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dCandTs, 0, cap / 64, TS_BLOCK_BYTES));
+    }
     h->candCap = cap;
     return RS_OK;
 }
@@ -662,28 +979,62 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
     hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H, h->W,
                        h->WD, h->M, h->dQf, h->dQsum);
+    if (h->planar)
+        hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H,
+                           h->M, h->dQp, h->dQsumRaw);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
 
-// Store raw staged queries src[i] into slots dst[i] of `lib`.
-int vt_store(rs_vt* h, uint4* lib, const uint8_t* d_raw, int n) {
+// Store raw staged queries src[i] into slots dst[i] of the library (or, with
+// `cand`, of the candidate buffer).
+int vt_store(rs_vt* h, bool cand, const uint8_t* d_raw, int n) {
     if (n == 0) return RS_OK;
+    uint4* lib = cand ? h->dCand : h->dLib;
     RS_HIP(hipMemcpyAsync(h->dSrc, h->hSrc, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
     RS_HIP(hipMemcpyAsync(h->dDst, h->hDst, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
     const int64_t total = (int64_t)n * h->WD * h->HQ;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(vt_store_kernel, dim3(grid), dim3(256), 0, h->stream, d_raw, h->dSrc,
                        h->dDst, n, lib, h->H, h->W, h->WD, h->HQ);
+    if (h->planar)
+        hipLaunchKernelGGL(vt_plane_store_kernel, dim3(n), dim3(256), 0, h->stream, d_raw, h->dSrc,
+                           h->dDst, h->H, h->M, cand ? h->dCandP : h->dLibP,
+                           cand ? h->dCandTs : h->dLibTs);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
 
 // Launch a scan of queries [0, nq) (forms in dQf) against `count` slots of lib.
 template <bool MATRIX>
-int vt_launch_scan(rs_vt* h, const uint4* lib, int64_t count, int nq, ScanOut out, int rank,
+int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
+                    int nranks) {
+    const int ntb = (int)((count + 63) / 64);
+    // One resident wave of blocks: nqc near-equal query chunks per template block so
+    // that ntb * nqc fills the block slots once (a multiple of 8 keeps the XCD-aware
+    // mapping exact).  Libraries beyond the slot count run ntb blocks of all queries.
+    int nqc = std::max(1, std::min(nq, h->planeSlots / ntb));
+    if (nqc >= 8) nqc &= ~7;
+    RS_CHECK((int64_t)ntb * nqc < (1ll << 31), RS_ERR_ARG, "scan grid too large");
+    const dim3 grid((unsigned)(ntb * nqc));
+    const uint4* planes = reinterpret_cast<const uint4*>(cand ? h->dCandP : h->dLibP);
+    const uint32_t* ts = cand ? h->dCandTs : h->dLibTs;
+    if (h->H == 64)
+        hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PL_CG), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, out, rank, nranks);
+    else
+        hipLaunchKernelGGL((vt_scan_plane_kernel<32, MATRIX>), grid, dim3(64 * PL_CG), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, out, rank, nranks);
+    RS_HIP(hipGetLastError());
+    return RS_OK;
+}
+
+template <bool MATRIX>
+int vt_launch_scan(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
                    int nranks) {
     if (count <= 0 || nq <= 0) return RS_OK;
+    if (h->planar) return vt_launch_plane<MATRIX>(h, cand, count, nq, out, rank, nranks);
+    const uint4* lib = cand ? h->dCand : h->dLib;
     const int ntb = (int)((count + 63) / 64);
     const bool fast = h->M == FAST_M && (h->H == 64 || h->H == 32);
     RS_CHECK((int64_t)ntb * nq < (1ll << 31), RS_ERR_ARG, "scan grid too large (%d x %d)", ntb, nq);
@@ -755,7 +1106,7 @@ int vt_append_staged(rs_vt* h, const std::vector<std::pair<int, int64_t>>& news)
         h->hDst[mine] = p.second / h->nranks;
         ++mine;
     }
-    RS_TRY(vt_store(h, h->dLib, h->dQraw, mine));
+    RS_TRY(vt_store(h, false, h->dQraw, mine));
     h->count = new_count;
     return RS_OK;
 }
@@ -777,7 +1128,7 @@ int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries) {
     const int64_t lc = local_count_of(h, h->count);
     ScanOut out{h->dBest, nullptr, 0};
     RS_HIP(hipEventRecord(h->ev0, h->stream));
-    RS_TRY(vt_launch_scan<false>(h, h->dLib, lc, nq, out, h->rank, h->nranks));
+    RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
     RS_HIP(hipEventRecord(h->ev1, h->stream));
     h->stagedQ = nq;
     return RS_OK;
@@ -820,11 +1171,11 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
             h->hDst[j] = j;
             cpos[cand[j]] = (int)j;
         }
-        RS_TRY(vt_store(h, h->dCand, h->dQraw, (int)C));
+        RS_TRY(vt_store(h, true, h->dQraw, (int)C));
         ldm = (int64_t)rs::round_up((size_t)C, 64);
         RS_TRY(vt_grow_matrix(h, (size_t)ldm * nq));
         ScanOut mo{nullptr, h->dMat, ldm};
-        RS_TRY(vt_launch_scan<true>(h, h->dCand, C, nq, mo, 0, 1));
+        RS_TRY(vt_launch_scan<true>(h, true, C, nq, mo, 0, 1));
         RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ldm * nq, hipMemcpyDeviceToHost,
                               h->stream));
         RS_HIP(hipStreamSynchronize(h->stream));
@@ -902,10 +1253,38 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
     h->H = H; h->W = W; h->M = max_offset; h->thr = thr; h->device = device;
     h->WD = (W + 3) / 4;
     h->HQ = (H + 3) / 4;
+    h->planar = W == 8 * PL_CG && (H == 64 || H == 32) && max_offset == FAST_M;
     if (const char* e = std::getenv("RS_VT_SCAN")) {
-        h->carry = std::strcmp(e, "carry") == 0;
+        // A/B switches for the byte-SWAR scans; "plane" (or unset) keeps the default
+        if (std::strcmp(e, "plane") != 0) h->planar = false;
+        h->carry = std::strcmp(e, "sad") != 0;
         if (std::strcmp(e, "rb2") == 0) h->scan_rb = 2;
         if (std::strcmp(e, "rb3") == 0) h->scan_rb = 3;
+    }
+    if (h->planar) {
+        // resident blocks per CU: the occupancy API, capped by the kernel's own VGPR and
+        // LDS arithmetic (the API has read one block high on gfx950 for some SGPR counts)
+        int per_cu = 0, cus = 0;
+        hipFuncAttributes fa{};
+        const void* fn = h->H == 64 ? reinterpret_cast<const void*>(vt_scan_plane_kernel<64, false>)
+                                    : reinterpret_cast<const void*>(vt_scan_plane_kernel<32, false>);
+        hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PL_CG, 0);
+        if (oe == hipSuccess) oe = hipFuncGetAttributes(&fa, fn);
+        if (oe == hipSuccess) oe = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (oe != hipSuccess) {
+            rs::set_error("occupancy query failed: %s", hipGetErrorString(oe));
+            delete h;
+            return RS_ERR_HIP;
+        }
+        const int vg = std::max(8, (fa.numRegs + 7) / 8 * 8);
+        const int by_vgpr = (512 / vg) * 4 / PL_CG;  // waves per SIMD x 4 SIMDs / waves per block
+        const int by_lds = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) : per_cu;
+        const int api = per_cu;
+        per_cu = std::max(1, std::min({api, by_vgpr, by_lds}));
+        if (std::getenv("RS_VT_DEBUG"))
+            std::fprintf(stderr, "plane scan: %d blocks/CU (api %d, vgpr %d [%d regs], lds %d) x %d CUs\n",
+                         per_cu, api, by_vgpr, fa.numRegs, by_lds, cus);
+        h->planeSlots = std::max(1, per_cu * cus);
     }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
@@ -932,7 +1311,9 @@ int rs_vt_destroy(rs_vt* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
-                    (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat})
+                    (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
+                    (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
+                    (void*)h->dQsumRaw})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat})
         if (p) (void)hipHostFree(p);
@@ -1062,7 +1443,7 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
     RS_TRY(vt_grow_matrix(h, (size_t)ld * nq));
     ScanOut mo{nullptr, h->dMat, ld};
     RS_HIP(hipEventRecord(h->ev0, h->stream));
-    RS_TRY(vt_launch_scan<true>(h, h->dLib, h->count, nq, mo, 0, 1));
+    RS_TRY(vt_launch_scan<true>(h, false, h->count, nq, mo, 0, 1));
     RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ld * nq, hipMemcpyDeviceToHost,
                           h->stream));

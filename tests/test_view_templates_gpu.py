@@ -79,6 +79,29 @@ def test_frozen_scan_vs_oracle(vtmod, t, q, h, w):
     assert len(lib.templates) == t
 
 
+@pytest.mark.parametrize('scan', ['plane', 'carry', 'sad', 'rb2', 'rb3'])
+@pytest.mark.parametrize('h', [64, 32])
+def test_scan_variants_vs_oracle(vtmod, monkeypatch, scan, h):
+    """Every scan form (RS_VT_SCAN; 'plane' is the default bit-plane scan) gives
+    the oracle's scores on the same inputs, including all-0 / all-255 extremes."""
+    monkeypatch.setenv('RS_VT_SCAN', scan)
+    rng = np.random.default_rng(h)
+    lib_np = V.synthetic_library(300, h, 32, seed=h + 1)
+    lib_np[5] = 0
+    lib_np[6] = 255
+    lib_np[7] = np.where(rng.random((h, 32)) < 0.5, 0, 255)
+    queries, _ = V.synthetic_queries(lib_np, 37, seed=h + 2)
+    queries[0] = 255
+    queries[1] = 0
+    lib = vtmod.ViewTemplates._from_shape((h, 32), 45000)
+    lib.add(lib_np)
+    ref = np.stack([V.vt_scores_library(lib_np, q) for q in queries])
+    assert np.array_equal(lib.scores(queries), ref)
+    idx, score, _ = lib.match_templates(queries, mode=0)
+    assert np.array_equal(score, ref.min(axis=1))
+    assert np.array_equal(idx, ref.argmin(axis=1))
+
+
 def test_all_pair_scores_vs_oracle(vtmod):
     lib_np = V.synthetic_library(150, 64, 32, seed=4)
     queries, _ = V.synthetic_queries(lib_np, 20, seed=5)
