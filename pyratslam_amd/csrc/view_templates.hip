@@ -557,7 +557,7 @@ constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
             unsigned hw_, xcc_;                                                            \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
-            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * PL_CG + (threadIdx.x >> 6)) * 6; \
+            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6; \
             d_[(slot) * 3 + 0] = __builtin_amdgcn_s_memrealtime();                         \
             d_[(slot) * 3 + 1] = __builtin_amdgcn_s_memtime();                             \
             d_[(slot) * 3 + 2] = ((unsigned long long)xcc_ << 32) | hw_;                   \
@@ -568,7 +568,7 @@ constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
     do {               \
     } while (0)
 #endif
-constexpr int PL_NB = PL_CG;   // queries per LDS reduction batch (one per wave)
+constexpr int PL_NB = 2;       // queries per LDS batch (staged planes; one reducing wave each)
 
 __device__ inline uint32_t plane_borrows(const uint32_t (&t)[8], const uint32_t* q) {
     uint32_t b = __builtin_amdgcn_bitop3_b32(t[0], q[0], 0u, 0x8E);
@@ -651,26 +651,40 @@ __global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restric
     if (threadIdx.x == 0) qsum[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
 }
 
+// Query start rows [M-3, H-M-1] are split into PL_SPLIT ranges, one wave each
+// per column group, so a wave keeps only the template units its rows meet
+// (10 of 16 at H = 64): fewer VGPRs, four waves per SIMD.
+constexpr int PL_SPLIT = 2;
+
+template <int H, int HALF>
+struct PlaneRange {
+    static constexpr int M = FAST_M, NU = H / 4, S0 = M - 3, S1 = H - M - 1, NS = S1 - S0 + 1;
+    static constexpr int NSH = (NS + PL_SPLIT - 1) / PL_SPLIT;
+    static constexpr int SA = S0 + HALF * NSH;
+    static constexpr int SB = (SA + NSH - 1) < S1 ? SA + NSH - 1 : S1;
+    static constexpr int ja(int s) { return (s - (M - 1)) > 0 ? (s - (M - 1) + 3) / 4 : 0; }
+    static constexpr int jb(int s) { return (s + (M - 1)) / 4 < NU - 1 ? (s + (M - 1)) / 4 : NU - 1; }
+    static constexpr int JLO = ja(SA), JHI = jb(SB), NUH = JHI - JLO + 1;
+};
+
 // One query start row S against the template units it meets (o = 4J - S within
 // +-(M-1): 3 or 4 units).  The borrow chains of those units are interleaved
 // plane by plane, so consecutive bitop3s are independent (a single chain would
 // stall on every instruction).  All indices are compile-time.
-template <int H, int S>
-__device__ __forceinline__ void plane_row(const uint32_t (&P)[H / 4][8], const uint32_t* q,
-                                          uint32_t (&acc)[2 * FAST_M - 1]) {
-    constexpr int M = FAST_M, NU = H / 4;
-    constexpr int JA = (S - (M - 1)) > 0 ? (S - (M - 1) + 3) / 4 : 0;  // first J with o >= -(M-1)
-    constexpr int JB0 = (S + (M - 1)) / 4;                             // last J with o <= M-1
-    constexpr int JB = JB0 < NU - 1 ? JB0 : NU - 1;
-    constexpr int NJ = JB - JA + 1;
-    static_assert(NJ >= 1 && NJ <= 4, "units per query row");
+template <int H, int HALF, int S>
+__device__ __forceinline__ void plane_row(const uint32_t (&P)[PlaneRange<H, HALF>::NUH][8],
+                                          const uint32_t* q, uint32_t (&acc)[2 * FAST_M - 1]) {
+    using R = PlaneRange<H, HALF>;
+    constexpr int M = FAST_M, JA = R::ja(S), JB = R::jb(S), NJ = JB - JA + 1;
+    static_assert(NJ >= 1 && NJ <= 4 && JA >= R::JLO && JB <= R::JHI, "units per query row");
     uint32_t b[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][0], q[0], 0u, 0x8E);
+    for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA - R::JLO + j][0], q[0], 0u, 0x8E);
 #pragma unroll
     for (int k = 1; k < 8; ++k)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][k], q[k], b[j], 0x8E);
+        for (int j = 0; j < NJ; ++j)
+            b[j] = __builtin_amdgcn_bitop3_b32(P[JA - R::JLO + j][k], q[k], b[j], 0x8E);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         // v_bcnt's own accumulator (asm keeps the compiler from re-associating
@@ -680,109 +694,123 @@ __device__ __forceinline__ void plane_row(const uint32_t (&P)[H / 4][8], const u
     }
 }
 
-// Query planes reach SGPRs in chunks of PL_QC rows, double-buffered: at a
-// chunk boundary wait for the chunk (scalar loads return out of order, so only
-// lgkmcnt(0) is exact), then issue the next chunk's loads, then compute; the
-// scheduling barriers keep the compiler from hoisting the next loads above the
-// wait, which would expose their latency on every row.
-constexpr int PL_QC = 4;
-constexpr unsigned WAIT_LGKM0 = 0xC07F;  // s_waitcnt lgkmcnt(0), vmcnt/expcnt untouched (gfx9)
-
-template <int H, int C>
-__device__ __forceinline__ void plane_load_chunk(const uint32_t* __restrict__ qf,
-                                                 uint32_t (&dst)[PL_QC * 8]) {
-    constexpr int NS = H - 2 * FAST_M + 3;
-#pragma unroll
-    for (int i = 0; i < PL_QC * 8; ++i)
-        if (C * PL_QC * 8 + i < NS * 8) dst[i] = qf[C * PL_QC * 8 + i];
+// Query planes are staged per batch in LDS and read as wave-uniform
+// ds_read_b128 broadcasts into VGPRs: on gfx950 a VALU instruction with an SGPR
+// operand issues at about half the all-VGPR rate (tools/ubench_chain.hip:
+// 0.23 vs 0.36-0.41 wave-instructions per SIMD-cycle), so the chains take both
+// operands from VGPRs.
+template <int H, int HALF, int S>
+__device__ __forceinline__ void plane_rows(const uint32_t (&P)[PlaneRange<H, HALF>::NUH][8],
+                                           const uint32_t* sq, uint32_t (&acc)[2 * FAST_M - 1]) {
+    using R = PlaneRange<H, HALF>;
+    const uint4 lo = *reinterpret_cast<const uint4*>(sq + (S - R::S0) * 8);
+    const uint4 hi = *reinterpret_cast<const uint4*>(sq + (S - R::S0) * 8 + 4);
+    const uint32_t q[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    plane_row<H, HALF, S>(P, q, acc);
+    if constexpr (S < R::SB) plane_rows<H, HALF, S + 1>(P, sq, acc);
 }
 
-template <int H, int S>
-__device__ __forceinline__ void plane_rows(const uint32_t (&P)[H / 4][8], const uint32_t* qf,
-                                           uint32_t (&qb)[2][PL_QC * 8],
-                                           uint32_t (&acc)[2 * FAST_M - 1]) {
-    constexpr int M = FAST_M, S0 = M - 3, S1 = H - M - 1, NS = S1 - S0 + 1;
-    constexpr int rel = S - S0, ci = rel / PL_QC, r = rel % PL_QC;
-    constexpr int NC = (NS + PL_QC - 1) / PL_QC;
-    if constexpr (r == 0) {
-        __builtin_amdgcn_s_waitcnt(WAIT_LGKM0);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (ci + 1 < NC) plane_load_chunk<H, ci + 1>(qf, qb[(ci + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    plane_row<H, S>(P, &qb[ci & 1][r * 8], acc);
-    if constexpr (S < S1) plane_rows<H, S + 1>(P, qf, qb, acc);
-}
+template <int H>
+struct PlaneLds {
+    static constexpr int M = FAST_M, NS = H - 2 * M + 3, NO = 2 * M - 1, NK = (NO + 1) / 2;
+    static constexpr int QW = PL_CG * NS * 8;                 // query-plane dwords per query
+    static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
+    uint4 q[PL_NB * QW / 4];                                   // the batch's query planes
+    uint32_t part[PL_NB][NK][NW][64];                          // u16 pairs: offsets 2k, 2k+1
+    uint32_t ts[16][64];                                       // TS(o) of the 64 templates
+    int batch;
+};
 
-template <int H, bool MATRIX>
-__global__ __launch_bounds__(64 * PL_CG) void vt_scan_plane_kernel(
-    const uint4* __restrict__ planes, const uint32_t* __restrict__ tsum, int ntb, int64_t count,
-    const uint32_t* __restrict__ qp, const uint32_t* __restrict__ qsum, int nq, int nqc,
-    ScanOut out, int rank, int nranks) {
-    constexpr int M = FAST_M, NU = H / 4, NO = 2 * M - 1, S0 = M - 3, S1 = H - M - 1;
-    constexpr int NS = S1 - S0 + 1, NK = (NO + 1) / 2;
-    __shared__ uint32_t s_part[PL_NB][NK][PL_CG][64];  // u16 pairs: offsets 2k, 2k+1
-    __shared__ uint32_t s_ts[16][64];
-    int tb, qk;
-    if (nqc >= 8) {  // XCD-aware: blocks b and b+8 share an XCD (and its L2)
-        const int j = blockIdx.x >> 3;
-        tb = j % ntb;
-        qk = (j / ntb) * 8 + (blockIdx.x & 7);
-    } else {
-        tb = blockIdx.x % ntb;
-        qk = blockIdx.x / ntb;
-    }
-    // chunk qk of nqc near-equal query ranges (sizes differ by at most one)
-    const int q0 = (int)((int64_t)qk * nq / nqc), q1 = (int)((int64_t)(qk + 1) * nq / nqc);
-    if (q0 >= q1) return;  // whole block: before any barrier
-    VT_STAMP(0);
-    const int cg = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 16 * 64; i += 64 * PL_CG)
-        s_ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
-    uint32_t P[NU][8];
+// The work of one wave: column group cg, query start rows of range HALF.
+template <int H, int HALF, bool MATRIX>
+__device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
+                                           int tb, int64_t count, const uint4* __restrict__ qp4,
+                                           const uint32_t* __restrict__ qsum, int nq,
+                                           unsigned* __restrict__ next_batch, ScanOut out,
+                                           int rank, int nranks, int wave, int cg, int lane) {
+    using R = PlaneRange<H, HALF>;
+    using LD = PlaneLds<H>;
+    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
+    uint32_t P[R::NUH][8];
     {
-        const uint4* src = planes + (size_t)(tb * PL_CG + cg) * NU * 128 + lane;
+        const uint4* src = planes + ((size_t)(tb * PL_CG + cg) * (H / 4) + R::JLO) * 128 + lane;
 #pragma unroll
-        for (int j = 0; j < NU; ++j) {
+        for (int j = 0; j < R::NUH; ++j) {
             const uint4 a = src[(2 * j) * 64], b = src[(2 * j + 1) * 64];
             P[j][0] = a.x; P[j][1] = a.y; P[j][2] = a.z; P[j][3] = a.w;
             P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
         }
     }
+    const int nbatch = (nq + PL_NB - 1) / PL_NB;
     const int64_t slot = (int64_t)tb * 64 + lane;
-    for (int qb = q0; qb < q1; qb += PL_NB) {
-        const int nb = min(PL_NB, q1 - qb);
+    const int tid = wave * 64 + lane;
+    for (;;) {
+        // two barriers per batch: (A) staged planes visible, (B) partial counts
+        // visible; the next batch is taken during the compute (L.batch is read
+        // before (A) and rewritten after it)
+        const int bi = L.batch;
+        if (bi >= nbatch) break;  // block-uniform
+        const int qb = bi * PL_NB, nb = min(PL_NB, nq - qb);
+        for (int i = tid; i < nb * LD::QW / 4; i += NT) L.q[i] = qp4[(size_t)qb * (LD::QW / 4) + i];
+        __syncthreads();  // (A)
+        if (tid == 0) L.batch = (int)atomicAdd(next_batch + tb, 1u);
 #pragma unroll 1
         for (int b = 0; b < nb; ++b) {
-            const int qi = qb + b;
-            const uint32_t* qf = qp + ((size_t)qi * PL_CG + cg) * NS * 8;
             uint32_t acc[NO];
 #pragma unroll
             for (int o = 0; o < NO; ++o) acc[o] = 0u;
-            uint32_t qb[2][PL_QC * 8];
-            plane_load_chunk<H, 0>(qf, qb[0]);
-            plane_rows<H, S0>(P, qf, qb, acc);
+            plane_rows<H, HALF, R::SA>(
+                P, reinterpret_cast<const uint32_t*>(L.q) + (b * PL_CG + cg) * NS * 8, acc);
 #pragma unroll
             for (int k = 0; k < NK; ++k)
-                s_part[b][k][cg][lane] = acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u);
+                L.part[b][k][wave][lane] = acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u);
         }
-        __syncthreads();
-        const int qi = qb + cg;  // wave cg finishes query qb + cg of the batch
-        if (qi < q1) {
+        __syncthreads();  // (B)
+        if (wave < nb) {  // wave w finishes query qb + w of the batch
+            const int qi = qb + wave;
             uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
             for (int k = 0; k < NK; ++k) {
                 uint32_t t = 0;  // per-half sums stay < 2^16: no carry between the halves
 #pragma unroll
-                for (int c = 0; c < PL_CG; ++c) t += s_part[cg][k][c][lane];
-                best = min(best, s_ts[2 * k][lane] + 256u * (t & 0xFFFFu));
-                if (2 * k + 1 < NO) best = min(best, s_ts[2 * k + 1][lane] + 256u * (t >> 16));
+                for (int w = 0; w < LD::NW; ++w) t += L.part[wave][k][w][lane];
+                best = min(best, L.ts[2 * k][lane] + 256u * (t & 0xFFFFu));
+                if (2 * k + 1 < NO) best = min(best, L.ts[2 * k + 1][lane] + 256u * (t >> 16));
             }
             emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
         }
-        __syncthreads();
     }
+}
+
+// nqc blocks serve each template block; they take query batches of PL_NB from
+// the template block's counter, so blocks that the SIMDs' oldest-first issue
+// favours take more batches and no SIMD is left running a lone straggler.
+template <int H, bool MATRIX>
+__global__ __launch_bounds__(64 * PL_CG * PL_SPLIT) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __restrict__ tsum,
+                          int ntb, int64_t count, const uint32_t* __restrict__ qp,
+                          const uint32_t* __restrict__ qsum, int nq, int nqc,
+                          unsigned* __restrict__ next_batch, ScanOut out, int rank, int nranks) {
+    static_assert(PL_SPLIT == 2, "two row ranges");
+    __shared__ PlaneLds<H> L;
+    const int tb = (nqc >= 8 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x) % ntb;  // XCD-aware
+    VT_STAMP(0);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, cg = wave % PL_CG, half = wave / PL_CG;
+    for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
+    if (threadIdx.x == 0) L.batch = (int)atomicAdd(next_batch + tb, 1u);
+    __syncthreads();
+    const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
+    if (half == 0)
+        plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, next_batch, out, rank, nranks,
+                                 wave, cg, lane);
+    else
+        plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, next_batch, out, rank, nranks,
+                                 wave, cg, lane);
+    // Each of the nqc blocks of a template block ends on exactly one failed take, so the
+    // block whose take returned nbatch + nqc - 1 is the counter's last user in this
+    // launch: it rewinds the counter for the next launch (no memset per scan).
+    if (threadIdx.x == 0 && L.batch == (nq + PL_NB - 1) / PL_NB + nqc - 1) next_batch[tb] = 0u;
     VT_STAMP(1);
 }
 
@@ -836,6 +864,8 @@ struct rs_vt {
     uint32_t* dQp = nullptr;
     uint32_t* dQsumRaw = nullptr;
     int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
+    unsigned* dCtr = nullptr;  // per template block: next query batch (plane scan)
+    int ctrCap = 0;
 };
 
 namespace {
@@ -1013,18 +1043,29 @@ int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int
     // One resident wave of blocks: nqc near-equal query chunks per template block so
     // that ntb * nqc fills the block slots once (a multiple of 8 keeps the XCD-aware
     // mapping exact).  Libraries beyond the slot count run ntb blocks of all queries.
-    int nqc = std::max(1, std::min(nq, h->planeSlots / ntb));
+    int nqc = std::max(1, std::min((nq + PL_NB - 1) / PL_NB, h->planeSlots / ntb));
     if (nqc >= 8) nqc &= ~7;
+    if (ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
+        const int cap = std::max(ntb, 2 * h->ctrCap);
+        if (h->dCtr) RS_HIP(hipFree(h->dCtr));
+        h->dCtr = nullptr;
+        h->ctrCap = 0;
+        RS_HIP(hipMalloc(&h->dCtr, sizeof(unsigned) * (size_t)cap));
+        RS_HIP(hipMemsetAsync(h->dCtr, 0, sizeof(unsigned) * (size_t)cap, h->stream));
+        h->ctrCap = cap;
+    }
     RS_CHECK((int64_t)ntb * nqc < (1ll << 31), RS_ERR_ARG, "scan grid too large");
     const dim3 grid((unsigned)(ntb * nqc));
     const uint4* planes = reinterpret_cast<const uint4*>(cand ? h->dCandP : h->dLibP);
     const uint32_t* ts = cand ? h->dCandTs : h->dLibTs;
     if (h->H == 64)
-        hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PL_CG), 0, h->stream,
-                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, out, rank, nranks);
+        hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PL_CG * PL_SPLIT), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, h->dCtr, out, rank,
+                           nranks);
     else
-        hipLaunchKernelGGL((vt_scan_plane_kernel<32, MATRIX>), grid, dim3(64 * PL_CG), 0, h->stream,
-                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, out, rank, nranks);
+        hipLaunchKernelGGL((vt_scan_plane_kernel<32, MATRIX>), grid, dim3(64 * PL_CG * PL_SPLIT), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, h->dCtr, out, rank,
+                           nranks);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
@@ -1268,7 +1309,7 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
         hipFuncAttributes fa{};
         const void* fn = h->H == 64 ? reinterpret_cast<const void*>(vt_scan_plane_kernel<64, false>)
                                     : reinterpret_cast<const void*>(vt_scan_plane_kernel<32, false>);
-        hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PL_CG, 0);
+        hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PL_CG * PL_SPLIT, 0);
         if (oe == hipSuccess) oe = hipFuncGetAttributes(&fa, fn);
         if (oe == hipSuccess) oe = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (oe != hipSuccess) {
@@ -1277,7 +1318,7 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
             return RS_ERR_HIP;
         }
         const int vg = std::max(8, (fa.numRegs + 7) / 8 * 8);
-        const int by_vgpr = (512 / vg) * 4 / PL_CG;  // waves per SIMD x 4 SIMDs / waves per block
+        const int by_vgpr = (512 / vg) * 4 / (PL_CG * PL_SPLIT);  // waves/SIMD x 4 SIMDs / waves/block
         const int by_lds = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) : per_cu;
         const int api = per_cu;
         per_cu = std::max(1, std::min({api, by_vgpr, by_lds}));
@@ -1313,7 +1354,7 @@ int rs_vt_destroy(rs_vt* h) {
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
                     (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
-                    (void*)h->dQsumRaw})
+                    (void*)h->dQsumRaw, (void*)h->dCtr})
         if (p) (void)hipFree(p);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat})
         if (p) (void)hipHostFree(p);

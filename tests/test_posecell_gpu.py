@@ -70,9 +70,9 @@ def test_random_odometry_vs_oracle(pcn, shape, steps):
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
 def test_mixed_shift_widths_vs_oracle(pcn, precision, tol):
-    """Steps with |ox| <= 4 take the WIDE path kernel (control and window fetched
-    together); faster steps (vtrans up to 2 m, |ox| up to 10) take the
-    control-dependent window.  Both must follow the oracle step for step."""
+    """Slow steps (|ox| <= 4) mixed with fast ones (vtrans up to 2 m, shifts up
+    to 10 cells, beyond the 7-tap window): the path kernel's shifted window
+    must follow the oracle step for step."""
     r = np.random.default_rng(21)
     od = np.stack([np.where(r.random(24) < 0.5, r.uniform(0, 0.8, 24), r.uniform(0.9, 2.0, 24)),
                    r.uniform(-0.15, 0.15, 24)], axis=1)
@@ -86,19 +86,6 @@ def test_mixed_shift_widths_vs_oracle(pcn, precision, tol):
         for s in range(len(od)):
             assert tuple(got[s]) == ref.update(od[s]), (shape, s)
         assert np.abs(net.posecells - ref.posecells).max() < tol
-
-
-def test_wide_window_bit_identical_to_narrow(pcn, monkeypatch):
-    """The WIDE variant changes only which rows are fetched, not the arithmetic."""
-    od = odometry(40, 23, vmax=0.8)
-    nets = []
-    for flag in ('0', '1'):
-        monkeypatch.setenv('RS_PC_NO_WIDE', flag)
-        n = pcn((64, 64, 36))
-        n.inject(1, (20, 40, 7))
-        nets.append((n.run(od), n.posecells))
-    assert np.array_equal(nets[0][0], nets[1][0])
-    assert np.array_equal(nets[0][1], nets[1][1])
 
 
 def test_large_grid_properties(pcn):
