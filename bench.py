@@ -33,6 +33,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+VALU_PEAK_GINSTS = 1024 * 2.4 * 0.5
+SCAN_KERNELS = {'plane': 'vt_scan_plane_kernel', 'carry': 'vt_scan_carry_kernel',
+                'sad': 'vt_scan_lane_kernel', 'rb2': 'vt_scan_rb_kernel', 'rb3': 'vt_scan_rb_kernel',
+                'generic': 'vt_scan_generic_kernel'}
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_COMPARE = 64 * 32  # one stored 64x32 u8 template
 METRIC = 'pose-cell steps/sec (64×64×36) + template-compares/sec at 1/2/4/8 GPU'
@@ -182,6 +186,7 @@ def bench_templates(args, d):
         'ms_per_step': 1e3 * dt / args.steps,
         'pcie_inclusive_value': compares * max(3, args.steps // 4) / dtp,
         'scan_ms': scan_ms,
+        'kernel': SCAN_KERNELS[vts.scan_form()],
         'compares_per_launch': float(T) * Q,
         'reduce': reduce_kind,
         'hits_correct': correct,
@@ -313,11 +318,24 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get('templates_per_gpu') == args.templates_per_gpu and tj.get('queries') == args.queries:
+            if (tj.get('templates_per_gpu') == args.templates_per_gpu and tj.get('queries') == args.queries
+                    and tj.get('kernel', '').startswith(tv['kernel'])):
                 roof['traffic'] = tj.get('hbm_bytes_per_launch')
                 roof['traffic_source'] = os.path.relpath(args.traffic_json, ROOT)
+                vi = tj.get('valu_insts_per_launch')
+                if vi:
+                    # the scan is VALU-bound: wave64 VALU issue peaks at one instruction per
+                    # 2 cycles per SIMD (1024 SIMDs, 2.4 GHz)
+                    ach = vi / (tv['scan_ms'] * 1e-3) / 1e9
+                    roof['valu'] = {'insts_per_launch': vi, 'achieved': ach,
+                                    'peak': VALU_PEAK_GINSTS, 'unit': 'G wave-instructions/s',
+                                    'frac': ach / VALU_PEAK_GINSTS}
         except Exception:
             pass
+    roof['note'] = ('achieved = 2,048 algorithmic bytes per compare (SURVEY.md 8(d)) / scan time; '
+                    'above the HBM peak because each template is read from HBM once per batch and '
+                    'reused from registers by all queries (traffic = measured HBM bytes per launch); '
+                    'the kernel is bound by VALU issue, see valu')
     out = {
         'metric': METRIC,
         'value': tv['value'],
@@ -345,7 +363,7 @@ def main():
         },
         'roofline': roof,
         'pose_cell': pc,
-        'template_scan': {'kernel_ms_per_launch': tv['scan_ms'],
+        'template_scan': {'kernel': tv['kernel'], 'kernel_ms_per_launch': tv['scan_ms'],
                           'pcie_inclusive_compares_per_s': tv['pcie_inclusive_value'],
                           'known_answer_hits_correct': tv['hits_correct']},
     }

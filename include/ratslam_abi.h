@@ -165,6 +165,10 @@ int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint6
                   int64_t* best_index, uint8_t* is_new);
 /* device time (ms) of the scan kernel in the last match call (HIP events) */
 int rs_vt_last_ms(rs_vt* h, double* ms);
+/* which scan kernel family the handle uses for its shape: "plane" (bit-plane
+ * borrow count, W == 32, H in {32, 64}, max_offset 8), "carry", "sad", "rb2",
+ * "rb3" (byte-SWAR forms, RS_VT_SCAN) or "generic"; NULL for a null handle */
+const char* rs_vt_scan_form(const rs_vt* h);
 
 /* Multi-GPU: one process per GPU, library sharded round-robin (template g lives
  * on rank g % nranks at slot g / nranks); per query the local first-argmin keys

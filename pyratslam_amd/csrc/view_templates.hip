@@ -726,7 +726,7 @@ template <int H, int HALF, bool MATRIX>
 __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
                                            int tb, int64_t count, const uint4* __restrict__ qp4,
                                            const uint32_t* __restrict__ qsum, int nq,
-                                           unsigned* __restrict__ next_batch, ScanOut out,
+                                           unsigned* __restrict__ ctr, int G, int g, ScanOut out,
                                            int rank, int nranks, int wave, int cg, int lane) {
     using R = PlaneRange<H, HALF>;
     using LD = PlaneLds<H>;
@@ -741,7 +741,8 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
             P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
         }
     }
-    const int nbatch = (nq + PL_NB - 1) / PL_NB;
+    // this block's query group g of G: batches g, g + G, g + 2G, ...
+    const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     const int64_t slot = (int64_t)tb * 64 + lane;
     const int tid = wave * 64 + lane;
     for (;;) {
@@ -750,10 +751,10 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
         // before (A) and rewritten after it)
         const int bi = L.batch;
         if (bi >= nbatch) break;  // block-uniform
-        const int qb = bi * PL_NB, nb = min(PL_NB, nq - qb);
+        const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
         for (int i = tid; i < nb * LD::QW / 4; i += NT) L.q[i] = qp4[(size_t)qb * (LD::QW / 4) + i];
         __syncthreads();  // (A)
-        if (tid == 0) L.batch = (int)atomicAdd(next_batch + tb, 1u);
+        if (tid == 0) L.batch = (int)atomicAdd(ctr, 1u);
 #pragma unroll 1
         for (int b = 0; b < nb; ++b) {
             uint32_t acc[NO];
@@ -793,24 +794,28 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
                           unsigned* __restrict__ next_batch, ScanOut out, int rank, int nranks) {
     static_assert(PL_SPLIT == 2, "two row ranges");
     __shared__ PlaneLds<H> L;
-    const int tb = (nqc >= 8 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x) % ntb;  // XCD-aware
+    // XCD-aware: blocks b and b+8 share an XCD (and its L2); with nqc >= 8 the query
+    // batches are split into 8 groups by XCD, so each L2 holds one group's planes
+    const int tb = (nqc >= 8 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x) % ntb;
+    const int G = nqc >= 8 ? 8 : 1, g = nqc >= 8 ? (int)(blockIdx.x & 7) : 0;
+    unsigned* ctr = next_batch + (size_t)tb * 8 + g;
     VT_STAMP(0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, cg = wave % PL_CG, half = wave / PL_CG;
     for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
-    if (threadIdx.x == 0) L.batch = (int)atomicAdd(next_batch + tb, 1u);
+    if (threadIdx.x == 0) L.batch = (int)atomicAdd(ctr, 1u);
     __syncthreads();
     const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
     if (half == 0)
-        plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, next_batch, out, rank, nranks,
+        plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
                                  wave, cg, lane);
     else
-        plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, next_batch, out, rank, nranks,
+        plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
                                  wave, cg, lane);
-    // Each of the nqc blocks of a template block ends on exactly one failed take, so the
-    // block whose take returned nbatch + nqc - 1 is the counter's last user in this
-    // launch: it rewinds the counter for the next launch (no memset per scan).
-    if (threadIdx.x == 0 && L.batch == (nq + PL_NB - 1) / PL_NB + nqc - 1) next_batch[tb] = 0u;
+    // Each of the nqc / G blocks sharing a counter ends on exactly one failed take, so
+    // the block whose take returned (group batches) + nqc / G - 1 is the counter's last
+    // user in this launch: it rewinds the counter for the next launch (no memset).
+    if (threadIdx.x == 0 && L.batch == ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G + nqc / G - 1) *ctr = 0u;
     VT_STAMP(1);
 }
 
@@ -864,7 +869,7 @@ struct rs_vt {
     uint32_t* dQp = nullptr;
     uint32_t* dQsumRaw = nullptr;
     int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
-    unsigned* dCtr = nullptr;  // per template block: next query batch (plane scan)
+    unsigned* dCtr = nullptr;  // per template block x query group: next batch (plane scan)
     int ctrCap = 0;
 };
 
@@ -1045,8 +1050,8 @@ int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int
     // mapping exact).  Libraries beyond the slot count run ntb blocks of all queries.
     int nqc = std::max(1, std::min((nq + PL_NB - 1) / PL_NB, h->planeSlots / ntb));
     if (nqc >= 8) nqc &= ~7;
-    if (ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
-        const int cap = std::max(ntb, 2 * h->ctrCap);
+    if (8 * ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
+        const int cap = std::max(8 * ntb, 2 * h->ctrCap);
         if (h->dCtr) RS_HIP(hipFree(h->dCtr));
         h->dCtr = nullptr;
         h->ctrCap = 0;
@@ -1493,6 +1498,15 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
     for (int q = 0; q < nq; ++q)
         for (int64_t t = 0; t < nt; ++t) scores[(size_t)q * nt + t] = h->hMat[(size_t)q * ld + t0 + t];
     return RS_OK;
+}
+
+const char* rs_vt_scan_form(const rs_vt* h) {
+    if (!h) return nullptr;
+    if (h->planar) return "plane";
+    if (h->M != FAST_M || (h->H != 64 && h->H != 32)) return "generic";
+    if (h->scan_rb == 2 && (h->H == 64 || h->H == 32)) return "rb2";
+    if (h->scan_rb == 3 && h->H == 64) return "rb3";
+    return h->carry ? "carry" : "sad";
 }
 
 int rs_vt_last_ms(rs_vt* h, double* ms) {

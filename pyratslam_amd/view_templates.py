@@ -206,6 +206,10 @@ class ViewTemplates:
         _lib.check(self._lib.rs_vt_last_ms(self._h, ctypes.byref(ms)))
         return ms.value
 
+    def scan_form(self):
+        """Scan kernel family used for this shape ('plane', 'carry', 'sad', ...)."""
+        return self._lib.rs_vt_scan_form(self._h).decode()
+
 
 class ShardedViewTemplates(ViewTemplates):
     """Template library sharded round-robin over ranks (template g on rank g % n).

@@ -7,7 +7,11 @@ FETCH_SIZE reports half of the bytes of a wide coalesced read on gfx950, so it
 is doubled: hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Infinity-cache
 hits are counted too, so this is an upper bound on DRAM bytes.
 
-usage: tools/pmc_summary.py --fetch DIR --write DIR --trace DIR --round r1 [--out profiles]
+SQ counters (optional --sq DIR): SQ_INSTS_VALU per dispatch (wave-instructions),
+the wave-cycle split (SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_INST_ANY + WAIT_ANY,
+quad-cycles) and GRBM_GUI_ACTIVE / 8 (cycles per XCD = the dispatch's clock span).
+
+usage: tools/pmc_summary.py --fetch DIR --write DIR --trace DIR [--sq DIR] --round r1 [--out profiles]
 """
 import argparse
 import collections
@@ -36,6 +40,7 @@ def main():
     ap.add_argument('--fetch', required=True)
     ap.add_argument('--write', required=True)
     ap.add_argument('--trace', required=True)
+    ap.add_argument('--sq', default=None)
     ap.add_argument('--round', default='r1')
     ap.add_argument('--out', default='profiles')
     ap.add_argument('--templates-per-gpu', type=int, default=1000)
@@ -43,6 +48,9 @@ def main():
     a = ap.parse_args()
     fetch = counters(a.fetch, 'FETCH_SIZE')
     write = counters(a.write, 'WRITE_SIZE')
+    sq_names = ('SQ_INSTS_VALU', 'SQ_INSTS_LDS', 'SQ_WAVE_CYCLES', 'SQ_ACTIVE_INST_ANY',
+                'SQ_WAIT_INST_ANY', 'SQ_WAIT_ANY', 'GRBM_GUI_ACTIVE')
+    sq = {c: counters(a.sq, c) for c in sq_names} if a.sq else {}
     stats = {}
     for r in csv.DictReader(open(os.path.join(a.trace, 'run_kernel_stats.csv'))):
         stats[short(r['Name'])] = {'calls': int(r['Calls']), 'avg_us': float(r['AverageNs']) / 1e3,
@@ -58,6 +66,14 @@ def main():
             wk = sum(w) / len(w)
             e.update({'fetch_kib_raw': fk, 'write_kib': wk,
                       'hbm_bytes_per_dispatch': (2 * fk + wk) * 1024, 'dispatches': len(f)})
+        sqk = {c: sum(v[k]) / len(v[k]) for c, v in sq.items() if v.get(k)}
+        if sqk:
+            e['sq'] = sqk
+            if 'SQ_WAVE_CYCLES' in sqk and sqk['SQ_WAVE_CYCLES'] > 0:
+                wc = sqk['SQ_WAVE_CYCLES']
+                e['wave_cycle_split'] = {n: sqk.get(c, 0) / wc for n, c in (
+                    ('issuing', 'SQ_ACTIVE_INST_ANY'), ('issue_stall', 'SQ_WAIT_INST_ANY'),
+                    ('waitcnt_or_barrier', 'SQ_WAIT_ANY'))}
         kernels[k] = e
     os.makedirs(a.out, exist_ok=True)
     summary = {'round': a.round, 'method': __doc__.strip().splitlines()[2:7], 'kernels': kernels}
@@ -68,6 +84,7 @@ def main():
         k = max(scan, key=lambda s: kernels[s]['dispatches'])
         with open(os.path.join(a.out, 'pmc_traffic.json'), 'w') as fh:
             json.dump({'kernel': k, 'hbm_bytes_per_launch': kernels[k]['hbm_bytes_per_dispatch'],
+                       'valu_insts_per_launch': kernels[k].get('sq', {}).get('SQ_INSTS_VALU'),
                        'templates_per_gpu': a.templates_per_gpu, 'queries': a.queries,
                        'source': f'{a.round}_pmc_summary.json'}, fh, indent=1)
     lines = [f'# rocprofv3 summary, round {a.round}', '',
