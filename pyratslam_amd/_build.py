@@ -13,6 +13,9 @@ INCLUDE = os.path.join(ROOT, 'include')
 LIB = os.path.join(HERE, 'libratslam_hip.so')
 OBJDIR = os.path.join(HERE, 'build')
 SOURCES = ['rs_common.cpp', 'posecell.hip', 'view_templates.hip']
+# per-source flags: the plane scan's batch takes are single-lane atomics; the
+# wave-aggregating atomic optimizer only adds a readfirstlane round trip to them
+EXTRA = {'view_templates.hip': ['-mllvm', '-amdgpu-atomic-optimizer-strategy=None']}
 HEADERS = [os.path.join(CSRC, 'rs_common.h'), os.path.join(INCLUDE, 'ratslam_abi.h')]
 ARCH = os.environ.get('PYRATSLAM_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
@@ -25,7 +28,7 @@ def _newer(src, dst):
 def build(verbose=False, force=False):
     """Compile every HIP/C++ source of the library and link it; returns the .so path."""
     os.makedirs(OBJDIR, exist_ok=True)
-    hdr_mtime = max(os.path.getmtime(h) for h in HEADERS)
+    hdr_mtime = max(os.path.getmtime(h) for h in HEADERS + [os.path.abspath(__file__)])
     objs = []
     for src in SOURCES:
         path = os.path.join(CSRC, src)
@@ -36,7 +39,7 @@ def build(verbose=False, force=False):
             continue
         lang = ['-x', 'hip'] if src.endswith('.hip') else []
         cmd = [HIPCC, f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-Wall',
-               '-Wno-unused-function', f'-I{INCLUDE}', f'-I{CSRC}', *lang, '-c', path, '-o', obj]
+               '-Wno-unused-function', f'-I{INCLUDE}', f'-I{CSRC}', *lang, *EXTRA.get(src, []), '-c', path, '-o', obj]
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.check_call(cmd)
