@@ -115,6 +115,9 @@ int rs_pc_last_ms(rs_pc* h, double* ms);
  * around every launch on the handle's stream; only when profiling is enabled) */
 int rs_pc_set_profiling(rs_pc* h, int enable);
 int rs_pc_kernel_ms(rs_pc* h, double ms[2]);
+/* step kernels in use: "rows" (row-tiled excite + path launches, Y <= 128) or
+ * "tiles" (3-D tiles, any Y) */
+const char* rs_pc_step_form(const rs_pc* h);
 
 /* ------------------------------------------------------------------------ */
 /* View templates                                                            */

@@ -14,8 +14,12 @@ LIB = os.path.join(HERE, 'libratslam_hip.so')
 OBJDIR = os.path.join(HERE, 'build')
 SOURCES = ['rs_common.cpp', 'posecell.hip', 'view_templates.hip']
 # per-source flags: the plane scan's batch takes are single-lane atomics; the
-# wave-aggregating atomic optimizer only adds a readfirstlane round trip to them
-EXTRA = {'view_templates.hip': ['-mllvm', '-amdgpu-atomic-optimizer-strategy=None']}
+# wave-aggregating atomic optimizer only adds a readfirstlane round trip to them.
+# The pose-cell stencils keep scalar FMAs: SLP packing into v_pk_fma_f32 pairs the
+# filter taps into register pairs and doubles the VGPRs of the conv_xy passes
+# (pc_fused_rows 90 -> 220, pc_path_rows<128> 85 -> 146), halving occupancy.
+EXTRA = {'view_templates.hip': ['-mllvm', '-amdgpu-atomic-optimizer-strategy=None'],
+         'posecell.hip': ['-fno-slp-vectorize']}
 HEADERS = [os.path.join(CSRC, 'rs_common.h'), os.path.join(INCLUDE, 'ratslam_abi.h')]
 ARCH = os.environ.get('PYRATSLAM_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

@@ -70,6 +70,7 @@ SIGNATURES = {
     'rs_pc_last_ms': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_set_profiling': (ctypes.c_int, [_vp, ctypes.c_int]),
     'rs_pc_kernel_ms': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_step_form': (ctypes.c_char_p, [_vp]),
     'rs_vt_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
     'rs_vt_destroy': (ctypes.c_int, [_vp]),

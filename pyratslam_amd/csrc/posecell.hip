@@ -1336,4 +1336,9 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
     return RS_OK;
 }
 
+const char* rs_pc_step_form(const rs_pc* h) {
+    if (!h) return nullptr;
+    return h->tiling ? "rows" : "tiles";
+}
+
 }  // extern "C"

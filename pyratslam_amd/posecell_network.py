@@ -210,6 +210,10 @@ class PoseCellNetwork:
         _lib.check(self._lib.rs_pc_last_ms(self._h, ctypes.byref(ms)))
         return ms.value
 
+    def step_form(self):
+        """Step kernels in use: 'rows' or 'tiles' (rs_pc_step_form)."""
+        return self._lib.rs_pc_step_form(self._h).decode()
+
     def set_profiling(self, enable=True):
         _lib.check(self._lib.rs_pc_set_profiling(self._h, int(bool(enable))))
 

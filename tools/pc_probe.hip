@@ -79,14 +79,15 @@ int main(int argc, char** argv) {
         }
     double ms = 0;
     rs_pc_last_ms(h, &ms);
-    printf("grid %dx%dx%d  tiling %d  blocks %d  run(%d): %.2f us/step\n", X, Y, TH, h->tiling,
-           h->nPart, n, 1e3 * ms / n);
+    printf("grid %dx%dx%d  form %s  blocks %d  run(%d): %.2f us/step\n", X, Y, TH,
+           rs_pc_step_form(h), h->nPart, n, 1e3 * ms / n);
     // stamps of the last step
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
     const int nb = h->nPart;
     for (int kid = 0; kid < 2; ++kid) {
-        const int ns = kid == 0 ? 4 : 6;
+        const int ns = kid == 0 ? 4 : (kid == 1 ? 6 : 7);
+        if (st[(size_t)kid * 4096 * 8] == 0) continue;  // kernel not used by this step form
         unsigned long long t0 = ~0ull, t1 = 0;
         std::vector<std::vector<double>> ph(ns);
         for (int b = 0; b < nb; ++b) {
@@ -99,7 +100,7 @@ int main(int argc, char** argv) {
         std::vector<double> starts;
         for (int b = 0; b < nb; ++b) starts.push_back((st[((size_t)kid * 4096 + b) * 8] - t0) * 10.0);
         printf("%s: first start -> last end %.2f us; start spread median %.2f max %.2f us\n",
-               kid == 0 ? "excite" : "path", (t1 - t0) * 1e-2, median(starts) * 1e-3,
+               kid == 0 ? "excite" : (kid == 1 ? "path" : "fused"), (t1 - t0) * 1e-2, median(starts) * 1e-3,
                *std::max_element(starts.begin(), starts.end()) * 1e-3);
         for (int i = 1; i < ns; ++i)
             printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph[i]) * 1e-3,
