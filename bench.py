@@ -53,6 +53,10 @@ def parse():
     ap.add_argument('--pc-steps', type=int, default=2000, help='timed pose-cell steps')
     ap.add_argument('--pc-warmup', type=int, default=200)
     ap.add_argument('--pc-calls', type=int, default=1000, help='timed per-call update()s')
+    ap.add_argument('--pc-stress-shape', default='128,128,72',
+                    help='configs[3] stencil-stress grid, reported beside the headline grid')
+    ap.add_argument('--pc-stress-steps', type=int, default=400)
+    ap.add_argument('--no-pc-stress', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=6.0, help='CPU baseline budget per leg')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
@@ -196,6 +200,44 @@ def bench_templates(args, d):
     return res
 
 
+def pc_roofline(ncell, per_step_kernel_ms):
+    alg = 24.0 * ncell            # 3 stencil passes x (read + write) x 4 B (SURVEY.md 8(d))
+    ach = alg / (per_step_kernel_ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': ach / HBM_PEAK_GBS, 'traffic': None,
+            'note': '24 B/cell/step algorithmic over the two kernels\' summed HIP-event time'}
+
+
+def bench_posecell_stress(args, d):
+    """configs[3]: the 128x128x72 grid, batched run() steps/s and kernel roofline."""
+    from pyratslam_amd import PoseCellNetwork, synthetic
+    shape = tuple(int(s) for s in args.pc_stress_shape.split(','))
+    net = PoseCellNetwork(shape, device=d.local)
+    net.inject(1, tuple(s // 2 for s in shape))
+    n = args.pc_stress_steps
+    od = synthetic.odometry(n + 50, seed=0)
+    net.run(od[:50])
+    d.barrier()
+    t0 = time.perf_counter()
+    net.run(od[50:50 + n])
+    t1 = time.perf_counter()
+    d.barrier()
+    dt = d.max(t1 - t0)
+    nprof = min(n, 200)
+    net.set_profiling(True)
+    net.run(od[:nprof])
+    ex_ms, pi_ms = net.kernel_ms()
+    net.set_profiling(False)
+    finite = bool(np.isfinite(net.posecells).all())
+    form = net.step_form()
+    net.close()
+    ncell = shape[0] * shape[1] * shape[2]
+    return {'shape': list(shape), 'steps_per_s': n / dt, 'us_per_step': 1e6 * dt / n,
+            'kernel_us_per_step': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
+            'step_form': form, 'finite': finite,
+            'roofline': pc_roofline(ncell, (ex_ms + pi_ms) / nprof)}
+
+
 def bench_posecells(args, d):
     from pyratslam_amd import PoseCellNetwork, synthetic
     shape = tuple(int(s) for s in args.pc_shape.split(','))
@@ -225,9 +267,12 @@ def bench_posecells(args, d):
     net.set_profiling(False)
     per_step_kernel_ms = (ex_ms + pi_ms) / nprof
     ncell = shape[0] * shape[1] * shape[2]
-    alg = 24.0 * ncell            # 3 stencil passes x (read + write) x 4 B (SURVEY.md 8(d))
     finite = bool(np.isfinite(net.posecells).all())
+    form = net.step_form()
     net.close()
+    roof = pc_roofline(ncell, per_step_kernel_ms)
+    roof['note'] += ('; the 576 KiB volume is L2-resident and the step is launch/latency-bound '
+                     'at this size (see pose_cell_stress for configs[3])')
     return {
         'shape': list(shape),
         'steps_per_s': args.pc_steps / dt,
@@ -235,14 +280,9 @@ def bench_posecells(args, d):
         'us_per_step': 1e6 * dt / args.pc_steps,
         'kernel_us_per_step': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
         'replicas': d.world,
+        'step_form': form,
         'finite': finite,
-        'roofline': {'bound': 'hbm', 'achieved': alg / (per_step_kernel_ms * 1e-3) / 1e9,
-                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': alg / (per_step_kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     'traffic': None,
-                     'note': '24 B/cell/step algorithmic over the two kernels\' summed '
-                             'HIP-event time; the 576 KiB volume is L2-resident and the '
-                             'step is launch/latency-bound at this size'},
+        'roofline': roof,
     }
 
 
@@ -305,6 +345,7 @@ def main():
     d = Dist(args.gpus)
     tv = bench_templates(args, d)
     pc = bench_posecells(args, d)
+    pcs = None if args.no_pc_stress else bench_posecell_stress(args, d)
     if d.rank != 0:
         d.close()
         return
@@ -363,6 +404,7 @@ def main():
         },
         'roofline': roof,
         'pose_cell': pc,
+        'pose_cell_stress': pcs,
         'template_scan': {'kernel': tv['kernel'], 'kernel_ms_per_launch': tv['scan_ms'],
                           'pcie_inclusive_compares_per_s': tv['pcie_inclusive_value'],
                           'known_answer_hits_correct': tv['hits_correct']},
