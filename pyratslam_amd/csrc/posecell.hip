@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -88,9 +90,20 @@ __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
             pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                               \
     } while (0)
+// shader-clock stamp (s_memtime) of thread 0, for per-phase cycle counts
+#define PC_STAMPC(kid, sid)                                                             \
+    do {                                                                                \
+        if (threadIdx.x == 0) {                                                         \
+            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                    \
+            pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memtime();     \
+        }                                                                               \
+    } while (0)
 #else
 #define PC_STAMP(kid, sid) \
     do {                   \
+    } while (0)
+#define PC_STAMPC(kid, sid) \
+    do {                    \
     } while (0)
 #endif
 
@@ -647,6 +660,423 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     PC_STAMP(1, 5);
 }
 
+// ---------------------------------------------------------------------------
+// Layer-streaming forms (the default).  A block of 8 waves owns BXB = BX*WR
+// rows x YT = 64*(8/WR) columns x KC layers of the output and walks its KC + 6
+// input layers in order.  Per input layer only 2-D work is done (window load
+// into double-buffered LDS, then the y and x passes or the 7x7 filter); the
+// 7-tap theta pass runs on a 7-deep register ring of per-lane results, so the
+// 2-D passes are evaluated (KC+6)/KC times per cell instead of the rows form's
+// (BK+6)/BK = 4x.  Lane <-> column; each wave register-blocks BX rows.
+// Window loads run ST_PF layers ahead of use (a 7-slot register ring, so the
+// slot of every stage is a compile-time index of the 7-way unrolled layer loop).
+// Every stage is straight-line: unconditional loads and LDS stores, and the
+// outputs go to an LDS buffer written back after the loop, so the only
+// vector-memory operations in the loop are the in-order window loads and the
+// compiler's vmcnt wait at each stage covers just that stage's slot (a global
+// store in flight makes it drain every prefetch).  The per-layer control
+// (shifts, filter index) and the filter table are staged in LDS once per block.
+// Tiles are numbered XCD-aware: dispatch is round-robin over the 8 XCDs, and
+// XCD x takes a contiguous run of tiles, so neighbouring tiles' halo rows and
+// layers meet in the same L2.
+// ---------------------------------------------------------------------------
+constexpr int ST_NT = 512, ST_NW = ST_NT / 64;
+#ifndef PC_ST_PF
+#define PC_ST_PF 3
+#endif
+constexpr int ST_PF = PC_ST_PF;           // window prefetch distance (layers)
+// The streaming grids hold 1-2 blocks per CU, so occupancy buys nothing: let the
+// scheduler spend registers on keeping LDS reads in flight (at the default
+// occupancy target it serialises every ds_read behind an lgkmcnt(0)).
+#ifndef PC_ST_WAVES
+#define PC_ST_WAVES __attribute__((amdgpu_waves_per_eu(1, 2)))
+#endif
+constexpr int ST_MAXKC = 12;              // layers per block (outputs buffered in LDS)
+constexpr int ST_MAXL = ST_MAXKC + 2 * 3 + ST_PF;  // control entries staged in LDS
+constexpr int ST_OUT_BYTES = 24 * 1024;   // LDS output buffer per block
+// layers per block that fit the output buffer for a tile of bxb x yt cells of esz bytes
+__host__ __device__ constexpr int st_maxkc(int esz, int bxb, int yt) {
+    return ST_OUT_BYTES / (esz * bxb * yt) < ST_MAXKC ? ST_OUT_BYTES / (esz * bxb * yt) : ST_MAXKC;
+}
+constexpr int ST_FTP = 52;                // filter stride in LDS: 49 taps padded to 13 x 16 B
+constexpr int NPP_MAX_BLOCKS = 4 * ST_NT * 64;
+constexpr size_t ST_MIN_CELLS = 512 * 1024;  // default form: streamed from this grid size
+static_assert(ST_PF >= 1 && ST_PF < FL, "prefetch ring has 7 slots");
+
+struct StreamGrid {  // tiles along x, y and theta chunks; layers per chunk
+    int gx, gy, gz, KC;
+};
+
+__device__ inline int st_tile(int b, int nb) {
+    if ((nb & 7) != 0) return b;
+    return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+// Window loads issued by hand.  The compiler's vmcnt pass cannot follow the
+// 7-slot register ring around the layer loop (it waits for every prefetch at
+// every stage, which collapses the pipeline to one layer), so the window loads
+// are inline asm (saddr form: wave-uniform layer base + 32-bit byte offset) and
+// each stage waits for exactly its own slot.  Nothing else in the loop touches
+// vector memory (outputs are buffered in LDS), and loads return in issue order.
+template <typename T>
+__device__ inline T st_load(const T* base, unsigned idx) {
+#ifdef PC_DIAG_NOLOAD  // diagnostic build of tools/pc_probe.hip only: no window traffic
+    return (T)(idx & 7) * (T)1e-3;
+#endif
+    T v;
+    const unsigned boff = idx * (unsigned)sizeof(T);
+    if constexpr (sizeof(T) == 4)
+        asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(boff), "s"(base) : "memory");
+    else
+        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(boff), "s"(base) : "memory");
+    return v;
+}
+// wait until at most N window loads are in flight; uses of v[] stay after the wait
+template <int N, typename T, int L>
+__device__ inline void st_wait(T (&v)[L]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+    for (int u = 0; u < L; ++u) asm volatile("" : "+v"(v[u]));
+}
+
+// Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
+// (:339-340) and the normalisation partial sum (:343), streamed over layers.
+template <typename T, int BX, int WR>
+__global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_excite_stream(const T* __restrict__ P, T* __restrict__ Q,
+                                                           double* __restrict__ part,
+                                                           unsigned long long* __restrict__ res_slot,
+                                                           int X, int Y, int TH, StreamGrid G,
+                                                           SepKernel<T> k) {
+    constexpr int WC = ST_NW / WR, YT = 64 * WC, BXB = BX * WR;
+    constexpr int HR = BXB + 2 * HALF, RW = YT + 2 * HALF, WN = HR * RW;
+    constexpr int LPT = (WN + ST_NT - 1) / ST_NT;
+    static_assert(ST_NW % WR == 0, "waves split into WR row groups x WC column tiles");
+    __shared__ T s_in[2][LPT * ST_NT];  // padded: every thread stores every stage
+    __shared__ T s_ye[2][HR * YT];
+    __shared__ T s_yi[2][HR * YT];
+    __shared__ T s_out[st_maxkc(sizeof(T), BXB, YT) * BXB * YT];
+    __shared__ double s_red[ST_NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = wave % WR, col = (wave / WR) * 64 + lane;
+    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int bx = tile % G.gx, rest = tile / G.gx;
+    const int i0 = bx * BXB, y0 = (rest % G.gy) * YT, k0 = (rest / G.gy) * G.KC;
+    const int nL = min(G.KC, TH - k0) + 2 * HALF;
+    const int gy = y0 + col;
+    PC_STAMP(2, 0);
+    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
+        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+
+    // window element e = (row r, col c) <-> P[L][(i0-3+r) % X][(y0-3+c) % Y]: the
+    // in-layer offset is fixed over layers
+    unsigned off[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+        const int e = min(tid + u * ST_NT, WN - 1), r = e / RW, c = e - r * RW;
+        off[u] = (unsigned)(rs::wrapi(i0 - HALF + r, X) * Y + rs::wrapi(y0 - HALF + c, Y));
+    }
+    const size_t lstride = (size_t)X * Y;
+    T pre[FL][LPT];
+#pragma unroll
+    for (int d = 0; d < ST_PF; ++d) {
+        const T* src = P + (size_t)rs::wrapi(k0 - HALF + d, TH) * lstride;
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) pre[d][u] = st_load(src, off[u]);
+    }
+
+    T re[FL][BX], ri[FL][BX];
+    double sum = 0.0;
+    PC_STAMP(2, 1);
+    for (int base = 0; base < nL; base += FL) {
+#pragma unroll
+        for (int s = 0; s < FL; ++s) {
+            const int it = base + s;
+            if (it >= nL) break;
+            const int b = it & 1;
+            if (it == 5) PC_STAMPC(4, 0);
+            st_wait<(ST_PF - 1) * LPT>(pre[s]);
+            if (it == 5) PC_STAMPC(4, 1);
+#pragma unroll
+            for (int u = 0; u < LPT; ++u) s_in[b][tid + u * ST_NT] = pre[s][u];
+            {  // layers past the chunk are valid (wrapped) addresses: no branch
+                const T* src = P + (size_t)rs::wrapi(k0 - HALF + it + ST_PF, TH) * lstride;
+#pragma unroll
+                for (int u = 0; u < LPT; ++u) pre[(s + ST_PF) % FL][u] = st_load(src, off[u]);
+            }
+            __syncthreads();
+            if (it == 0) PC_STAMP(2, 2);
+            if (it == 5) PC_STAMPC(4, 2);
+            // y pass: window rows rg, rg + WR, ... (both Gaussians share the loads)
+            for (int r = rg; r < HR; r += WR) {
+                const T* rw = &s_in[b][r * RW + col];
+                T e = 0, g = 0;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) {
+                    const T x = rw[t];
+                    e += k.ge[t] * x;
+                    g += k.gi[t] * x;
+                }
+                s_ye[b][r * YT + col] = e;
+                s_yi[b][r * YT + col] = g;
+            }
+            if (it == 5) PC_STAMPC(4, 3);
+            __syncthreads();
+            if (it == 5) PC_STAMPC(4, 4);
+            // x pass: this wave's BX rows, register-blocked over the BX + 6 window rows
+            T ye[BX + 2 * HALF], yi[BX + 2 * HALF];
+#pragma unroll
+            for (int a = 0; a < BX + 2 * HALF; ++a) {
+                ye[a] = s_ye[b][(rg * BX + a) * YT + col];
+                yi[a] = s_yi[b][(rg * BX + a) * YT + col];
+            }
+#pragma unroll
+            for (int i = 0; i < BX; ++i) {
+                T e = 0, g = 0;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) {
+                    e += k.ge[t] * ye[i + t];
+                    g += k.gi[t] * yi[i + t];
+                }
+                re[s][i] = e;
+                ri[s][i] = g;
+            }
+            if (it == 5) PC_STAMPC(4, 5);
+            // theta pass over the ring (input it-6+t sits in slot (s+1+t) % 7),
+            // relu(v - inhib), partial sum; the output waits in LDS
+            if (it >= 2 * HALF) {
+                const int o = it - 2 * HALF;
+#pragma unroll
+                for (int i = 0; i < BX; ++i) {
+                    T e = 0, g = 0;
+#pragma unroll
+                    for (int t = 0; t < FL; ++t) {
+                        e += k.ge[t] * re[(s + 1 + t) % FL][i];
+                        g += k.gi[t] * ri[(s + 1 + t) % FL][i];
+                    }
+                    const T v = (e - g) * k.scale;
+                    const T q = (v < k.inhib) ? T(0) : v - k.inhib;
+                    s_out[(o * BXB + rg * BX + i) * YT + col] = q;
+                    if (i0 + rg * BX + i < X && gy < Y) sum += (double)q;
+                }
+            }
+            if (it == 5) PC_STAMPC(4, 6);
+        }
+    }
+    PC_STAMP(2, 3);
+    // write-back: each thread stores the cells it computed (its own LDS slots)
+    for (int o = 0; o < nL - 2 * HALF; ++o)
+#pragma unroll
+        for (int i = 0; i < BX; ++i) {
+            const int gi = i0 + rg * BX + i;
+            if (gi < X && gy < Y)
+                Q[((size_t)(k0 + o) * X + gi) * Y + gy] = s_out[(o * BXB + rg * BX + i) * YT + col];
+        }
+    sum = block_sum_w<ST_NW>(sum, s_red);
+    if (tid == 0) part[blockIdx.x] = sum;
+    PC_STAMP(2, 4);
+}
+
+// 49 filter taps from LDS (uniform address: broadcast reads, 16 B each for float)
+template <typename T>
+__device__ inline void st_filter(const T* __restrict__ src, T (&f)[FT]) {
+    if constexpr (sizeof(T) == 4) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+#pragma unroll
+        for (int q = 0; q < ST_FTP / 4; ++q) {
+            const float4 v = s4[q];
+            if (4 * q + 0 < FT) f[4 * q + 0] = v.x;
+            if (4 * q + 1 < FT) f[4 * q + 1] = v.y;
+            if (4 * q + 2 < FT) f[4 * q + 2] = v.z;
+            if (4 * q + 3 < FT) f[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < FT; ++t) f[t] = src[t];
+    }
+}
+
+// Path integration (posecell_network.py:252-314): per-layer shifted 7x7 filter
+// (:273 -> convolution.py:320-340), clamp (:300), 7-tap theta filter (:310 ->
+// convolution.py:344-359), clamp (:314), normalisation by the excitation total
+// (:343-345, applied at the end), fused argmax (:317-319), streamed over layers.
+template <typename T, int BX, int WR, typename CTL>
+__global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
+    const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
+    const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
+    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, StreamGrid G) {
+    constexpr int WC = ST_NW / WR, YT = 64 * WC, BXB = BX * WR;
+    constexpr int HR = BXB + 2 * HALF, RW = YT + 2 * HALF, WN = HR * RW;
+    constexpr int LPT = (WN + ST_NT - 1) / ST_NT;
+    constexpr int NPP = 4;  // normalisation partials per thread (npart <= NPP * ST_NT)
+    static_assert(ST_NW % WR == 0, "waves split into WR row groups x WC column tiles");
+    __shared__ T s_win[2][LPT * ST_NT];  // padded: every thread stores every stage
+    __shared__ T s_out[st_maxkc(sizeof(T), BXB, YT) * BXB * YT];
+    __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
+    __shared__ int s_ox[ST_MAXL], s_oy[ST_MAXL], s_fo[ST_MAXL];
+    __shared__ double s_red[ST_NW];
+    __shared__ T s_bv[ST_NW];
+    __shared__ unsigned s_bl[ST_NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int rg = wave % WR, col = (wave / WR) * 64 + lane;
+    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int bx = tile % G.gx, rest = tile / G.gx;
+    const int i0 = bx * BXB, y0 = (rest % G.gy) * YT, k0 = (rest / G.gy) * G.KC;
+    const int nL = min(G.KC, TH - k0) + 2 * HALF;
+    const int gy = y0 + col;
+    const size_t lstride = (size_t)X * Y;
+    PC_STAMP(3, 0);
+
+    // stage the block's control and the filter table; issue the normalisation
+    // partials' loads (reduced after the first windows are in flight)
+    if (tid < nL + ST_PF) {  // + the prefetches issued past the chunk
+        const int L = rs::wrapi(k0 - HALF + tid, TH);
+        s_ox[tid] = rs::wrapi(ctl_ox(ctl, L), X);   // shifts may exceed the grid (vtrans large)
+        s_oy[tid] = rs::wrapi(ctl_oy(ctl, L), Y);
+        s_fo[tid] = ctl_fi(ctl, L) * ST_FTP;
+    }
+    for (int i = tid; i < nf * FT; i += ST_NT) {
+        const int fi = i / FT;
+        s_ftab[fi * ST_FTP + (i - fi * FT)] = filt[i];
+    }
+    double pt[NPP];
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) {
+        const int i = tid + u * ST_NT;
+        pt[u] = i < npart ? part[i] : 0.0;
+    }
+    double pextra = 0.0;
+    for (int i = tid + NPP * ST_NT; i < npart; i += ST_NT) pextra += part[i];
+    T zf[FL];
+#pragma unroll
+    for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
+    __syncthreads();
+
+    // window element e = (row r, col c) <-> Q[L][(i0-3+r+ox[L]) % X][(y0-3+c+oy[L]) % Y]
+    // unshifted window coordinates, wrapped once: (a + o) % n == (a % n + o) % n with
+    // o in [0, n), so a shifted coordinate needs one conditional subtraction
+    int er[LPT], ec[LPT];
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+        const int e = min(tid + u * ST_NT, WN - 1), r = e / RW;
+        er[u] = rs::wrapi(i0 - HALF + r, X);
+        ec[u] = rs::wrapi(y0 - HALF + (e - r * RW), Y);
+    }
+    T pre[FL][LPT];
+    auto load = [&](int it, T(&dst)[LPT]) {
+        const int ox = s_ox[it], oy = s_oy[it];
+        const T* src = Q + (size_t)rs::wrapi(k0 - HALF + it, TH) * lstride;
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            int gx = er[u] + ox, gc = ec[u] + oy;
+            gx -= gx >= X ? X : 0;
+            gc -= gc >= Y ? Y : 0;
+            dst[u] = st_load(src, (unsigned)(gx * Y + gc));
+        }
+    };
+#pragma unroll
+    for (int d = 0; d < ST_PF; ++d) load(d, pre[d]);
+    double tot = pextra;
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) tot += pt[u];
+    tot = block_sum_w<ST_NW>(tot, s_red);
+    const T tt = (T)tot;
+
+    T ring[FL][BX];
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    PC_STAMP(3, 1);
+    for (int base = 0; base < nL; base += FL) {
+#pragma unroll
+        for (int s = 0; s < FL; ++s) {
+            const int it = base + s;
+            if (it >= nL) break;
+            const int b = it & 1;
+            st_wait<(ST_PF - 1) * LPT>(pre[s]);
+#pragma unroll
+            for (int u = 0; u < LPT; ++u) s_win[b][tid + u * ST_NT] = pre[s][u];
+            load(it + ST_PF, pre[(s + ST_PF) % FL]);  // straight line: see pc_excite_stream
+            __syncthreads();
+            if (it == 0) PC_STAMP(3, 2);
+            T f[FT];
+            st_filter<T>(s_ftab + s_fo[it], f);
+            T acc[BX];
+#pragma unroll
+            for (int i = 0; i < BX; ++i) acc[i] = 0;
+#pragma unroll
+            for (int a = 0; a < BX + 2 * HALF; ++a) {
+                T w[FL];
+                const T* rw = &s_win[b][(rg * BX + a) * RW + col];
+#pragma unroll
+                for (int t = 0; t < FL; ++t) w[t] = rw[t];
+#pragma unroll
+                for (int i = 0; i < BX; ++i) {
+                    const int x = a - i;
+                    if (x < 0 || x >= FL) continue;
+#pragma unroll
+                    for (int t = 0; t < FL; ++t) acc[i] += w[t] * f[x * FL + t];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < BX; ++i) ring[s][i] = acc[i] > T(0) ? acc[i] : T(0);
+            if (it >= 2 * HALF) {
+                const int o = it - 2 * HALF, gk = k0 + o;
+#pragma unroll
+                for (int i = 0; i < BX; ++i) {
+                    T v = 0;
+#pragma unroll
+                    for (int z = 0; z < FL; ++z) v += ring[(s + 1 + z) % FL][i] * zf[z];
+                    v = v > T(0) ? v : T(0);
+                    if (tot != 0.0) v = v / tt;
+                    s_out[(o * BXB + rg * BX + i) * YT + col] = v;
+                    const int gi = i0 + rg * BX + i;
+                    const unsigned lin = ((unsigned)gi * Y + gy) * TH + gk;
+                    if (gi < X && gy < Y && (v > bv || (v == bv && lin < bl))) {
+                        bv = v;
+                        bl = lin;
+                    }
+                }
+            }
+        }
+    }
+    PC_STAMP(3, 3);
+    // write-back: each thread stores the cells it computed (its own LDS slots)
+    for (int o = 0; o < nL - 2 * HALF; ++o)
+#pragma unroll
+        for (int i = 0; i < BX; ++i) {
+            const int gi = i0 + rg * BX + i;
+            if (gi < X && gy < Y)
+                P[((size_t)(k0 + o) * X + gi) * Y + gy] = s_out[(o * BXB + rg * BX + i) * YT + col];
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const T ov = __shfl_xor(bv, off);
+        const unsigned ol = __shfl_xor(bl, off);
+        if (ov > bv || (ov == bv && ol < bl)) {
+            bv = ov;
+            bl = ol;
+        }
+    }
+    if (lane == 0) {
+        s_bv[wave] = bv;
+        s_bl[wave] = bl;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < ST_NW; ++w)
+            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                bv = s_bv[w];
+                bl = s_bl[w];
+            }
+        if constexpr (sizeof(T) == 4) {
+            atomicMax(res_slot + (blockIdx.x & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
+        } else {
+            bmax[blockIdx.x] = bv;
+            bidx[blockIdx.x] = bl;
+        }
+    }
+    PC_STAMP(3, 4);
+}
+
 // One block reduces per-block (value, index) argmax partials into the packed slot.
 template <typename T>
 __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ bmax,
@@ -837,6 +1267,9 @@ struct rs_pc {
     std::vector<hipEvent_t> evPool;
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
+    bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
+    int sbx = 1, swr = 8;  // streaming tile: BX rows per wave, WR row groups
+    StreamGrid sg{};
 };
 
 namespace {
@@ -937,6 +1370,44 @@ PcCtlRing make_ctl_ring(const rs_pc* h, int s) {
                      reinterpret_cast<const double*>(rec + ctl_off_zf(h))};
 }
 
+// Streaming variants instantiated: (BX rows per wave, WR row groups of waves).
+#define PC_STREAM_VARIANTS(X_) X_(1, 8) X_(2, 8) X_(1, 4) X_(2, 4)
+
+template <typename T, typename CTL>
+int pc_launch_stream(rs_pc* h, const T* P, T* Q, unsigned long long* slot, T* bmax, unsigned* bidx,
+                     const CTL* ctl, int prof_base) {
+    const StreamGrid G = h->sg;
+    const dim3 grid(G.gx * G.gy * G.gz), block(ST_NT);
+    const SepKernel<T>& k = sep_of<T>(h);
+    const T* filt = static_cast<const T*>(h->dFilt);
+    bool done = false;
+#define PC_EXCITE_CASE(bx_, wr_)                                                              \
+    if (!done && h->sbx == bx_ && h->swr == wr_) {                                            \
+        hipLaunchKernelGGL((pc_excite_stream<T, bx_, wr_>), grid, block, 0, h->stream, P, Q,   \
+                           h->dPart, slot, h->X, h->Y, h->TH, G, k);                          \
+        done = true;                                                                          \
+    }
+    PC_STREAM_VARIANTS(PC_EXCITE_CASE)
+#undef PC_EXCITE_CASE
+    RS_CHECK(done, RS_ERR_STATE, "no streaming variant BX=%d WR=%d", h->sbx, h->swr);
+    RS_HIP(hipGetLastError());
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+    if (!ctl) return RS_OK;
+    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+    done = false;
+#define PC_PATH_CASE(bx_, wr_)                                                                   \
+    if (!done && h->sbx == bx_ && h->swr == wr_) {                                               \
+        hipLaunchKernelGGL((pc_path_stream<T, bx_, wr_, CTL>), grid, block, 0, h->stream, Q,      \
+                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,  \
+                           bmax, bidx, h->X, h->Y, h->TH, G);                                    \
+        done = true;                                                                             \
+    }
+    PC_STREAM_VARIANTS(PC_PATH_CASE)
+#undef PC_PATH_CASE
+    RS_HIP(hipGetLastError());
+    return RS_OK;
+}
+
 template <typename T, typename CTL>
 int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     const T* P = static_cast<const T*>(h->dP);
@@ -947,7 +1418,9 @@ int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     unsigned* bidx = h->dArgI ? h->dArgI + (size_t)s * h->nPathBlocks : nullptr;
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
-    if (h->tiling == 64 || h->tiling == 128) {
+    if (h->streamed) {
+        RS_TRY((pc_launch_stream<T, CTL>(h, P, Q, slot, bmax, bidx, ctl, prof_base)));
+    } else if (h->tiling == 64 || h->tiling == 128) {
         const dim3 g((h->X + RT_BX - 1) / RT_BX, (h->TH + RT_BK - 1) / RT_BK);
         if (h->tiling == 64)
             hipLaunchKernelGGL((pc_excite_rows<T, 64>), g, dim3(RT_NT), 0, h->stream, P, Q,
@@ -1101,6 +1574,109 @@ __global__ void pc_scale_kernel(T* __restrict__ P, size_t n, const double* __res
         P[e] = P[e] / tt;
 }
 
+// Step-kernel form.  Default: layer streaming with one wave per 64 columns and
+// 8 row groups of BX rows; KC (layers per block) is the smallest chunk that keeps
+// the grid within ~2 blocks per CU (fewer, longer blocks re-evaluate fewer halo
+// layers).  RS_PC_FORM=rows|tiles|stream:BX,WR[,KC] overrides (A/B, tests).
+// The streaming kernels count their own window loads with explicit vmcnt waits,
+// which is only sound when the compiler puts no other vector-memory traffic in
+// the layer loop: refuse a variant that spills to scratch.
+template <typename T>
+int pc_stream_scratch(int bx, int wr, size_t* bytes) {
+    hipFuncAttributes a{};
+    *bytes = 0;
+    bool done = false;
+#define PC_SCRATCH(bx_, wr_)                                                                 \
+    if (!done && bx == bx_ && wr == wr_) {                                                   \
+        const void* fns[3] = {reinterpret_cast<const void*>(&pc_excite_stream<T, bx_, wr_>), \
+                              reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, PcCtlRing>), \
+                              reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, PcCtlInline>)}; \
+        for (const void* f : fns) {                                                          \
+            RS_HIP(hipFuncGetAttributes(&a, f));                                             \
+            *bytes += a.localSizeBytes;                                                      \
+        }                                                                                    \
+        done = true;                                                                         \
+    }
+    PC_STREAM_VARIANTS(PC_SCRATCH)
+#undef PC_SCRATCH
+    return RS_OK;
+}
+
+int pc_choose_form(rs_pc* h) {
+    int bx = 1, wr = 8, kc = 0;
+    const char* env = std::getenv("RS_PC_FORM");
+    if (env && std::strcmp(env, "rows") == 0) {
+        RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=rows needs Y <= 128");
+        h->streamed = false;
+        return RS_OK;
+    }
+    if (env && std::strcmp(env, "tiles") == 0) {
+        h->streamed = false;
+        h->tiling = 0;
+        return RS_OK;
+    }
+    if (env && std::strncmp(env, "stream:", 7) == 0) {
+        const int n = std::sscanf(env + 7, "%d,%d,%d", &bx, &wr, &kc);
+        RS_CHECK(n >= 2, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR[,KC], got '%s'", env);
+    } else {
+        RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
+                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR[,KC]])", env);
+        // default: one pass per kernel (rows) while the whole grid fits in one wave of
+        // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
+        // streamed); streamed once the rows form's 4x theta-halo recompute dominates
+        // (128x128x72: 57 us rows vs 42 us streamed, bx 2)
+        const bool big = (size_t)h->X * h->Y * h->TH >= ST_MIN_CELLS;
+        if ((env == nullptr || env[0] == 0) && h->tiling != 0 && !big) {
+            h->streamed = false;
+            return RS_OK;
+        }
+        bx = h->esz == 4 ? 2 : 1;
+    }
+    if (h->nf > RT_NFMAX) {  // filter table too large to stage in LDS: rows / tiles forms
+        RS_CHECK(env == nullptr || std::strncmp(env, "stream", 6) != 0, RS_ERR_ARG,
+                 "stream form stages at most %d path filters, table has %d", RT_NFMAX, h->nf);
+        h->streamed = false;
+        return RS_OK;
+    }
+    const int bxb = bx * wr, yt = 64 * (ST_NW / (wr > 0 ? wr : 1));
+    StreamGrid g;
+    g.gx = (h->X + bxb - 1) / bxb;
+    g.gy = (h->Y + yt - 1) / yt;
+    bool known = false;
+#define PC_KNOWN(bx_, wr_) known = known || (bx == bx_ && wr == wr_);
+    PC_STREAM_VARIANTS(PC_KNOWN)
+#undef PC_KNOWN
+    RS_CHECK(known, RS_ERR_ARG, "no streaming variant BX=%d WR=%d", bx, wr);
+    size_t scratch = 0;
+    if (h->esz == 4)
+        RS_TRY(pc_stream_scratch<float>(bx, wr, &scratch));
+    else
+        RS_TRY(pc_stream_scratch<double>(bx, wr, &scratch));
+    RS_CHECK(scratch == 0, RS_ERR_ARG,
+             "streaming variant BX=%d WR=%d spills %zu B to scratch at this precision", bx, wr,
+             scratch);
+    if (kc <= 0) {
+        // smallest chunk that keeps the grid within one block per CU (fewer, longer
+        // blocks re-evaluate fewer halo layers)
+        const int target = 256;
+        kc = 2;
+        while (kc < ST_MAXKC && kc < h->TH && (long)g.gx * g.gy * ((h->TH + kc - 1) / kc) > target) ++kc;
+    }
+    const int maxkc = st_maxkc((int)h->esz, bxb, yt);
+    if (kc > maxkc && (env == nullptr || std::strncmp(env, "stream:", 7) != 0)) kc = maxkc;
+    RS_CHECK(kc >= 1 && kc <= maxkc, RS_ERR_ARG, "stream KC=%d outside [1, %d]", kc, maxkc);
+    if (kc > h->TH) kc = h->TH;
+    g.KC = kc;
+    g.gz = (h->TH + g.KC - 1) / g.KC;
+    RS_CHECK((long)g.gx * g.gy * g.gz <= NPP_MAX_BLOCKS, RS_ERR_ARG,
+             "streaming grid of %ld blocks exceeds %d", (long)g.gx * g.gy * g.gz, NPP_MAX_BLOCKS);
+    h->streamed = true;
+    h->sbx = bx;
+    h->swr = wr;
+    h->sg = g;
+    return RS_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -1134,7 +1710,14 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     fill_sep(h->kd, p);
     h->ctlStride = rs::round_up(ctl_off_zf(h) + sizeof(double) * 8, 16);
     h->tiling = Y <= 64 ? 64 : (Y <= 128 ? 128 : 0);
-    if (h->tiling) {
+    if (int st = pc_choose_form(h); st != RS_OK) {
+        delete h;
+        return st;
+    }
+    if (h->streamed) {
+        h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;
+        h->nPathBlocks = h->nPart;
+    } else if (h->tiling) {
         h->nPart = ((X + RT_BX - 1) / RT_BX) * ((TH + RT_BK - 1) / RT_BK);
         h->nPathBlocks = h->nPart;
     } else {
@@ -1338,6 +1921,7 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
 
 const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
+    if (h->streamed) return "stream";
     return h->tiling ? "rows" : "tiles";
 }
 

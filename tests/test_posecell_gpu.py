@@ -185,3 +185,44 @@ def test_simulate_driver(pcn):
     for s in range(40):
         sim.step()
         assert sim.current_pose_cell == tuple(case['max_pc'][s])
+
+
+# every step-kernel form (RS_PC_FORM) against the oracle: the row-tiled and 3-D
+# tiled single-pass forms and the layer-streaming form at several tile shapes
+# (rows per wave, row groups, layers per block), incl. ragged tiles and grids
+# whose theta extent is not a multiple of the chunk
+FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,2', 'stream:1,8,5', 'stream:2,8,3',
+                     'stream:1,4,3', 'stream:2,4,6'],
+         'float64': ['rows', 'tiles', 'stream:1,8,2', 'stream:1,8,5', 'stream:1,4,3']}
+
+
+@pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
+def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
+    od = odometry(10, 17)
+    for shape in ((64, 64, 36), (21, 21, 36), (24, 40, 13), (70, 100, 20)):
+        loc = tuple(s // 2 for s in shape)
+        ref = P.PoseCellOracle(shape)
+        ref.inject(1, loc)
+        maxes = [ref.update(v) for v in od]
+        want = ref.posecells
+        for form in FORMS[precision]:
+            monkeypatch.setenv('RS_PC_FORM', form)
+            net = pcn(shape, precision=precision)
+            assert net.step_form() == form.split(':')[0]
+            net.inject(1, loc)
+            got = net.run(od)
+            assert [tuple(m) for m in got] == maxes, (shape, form)
+            assert np.abs(net.posecells - want).max() < tol, (shape, form)
+            net.close()
+
+
+def test_default_form_by_grid_size(pcn, monkeypatch):
+    monkeypatch.delenv('RS_PC_FORM', raising=False)
+    assert pcn((64, 64, 36)).step_form() == 'rows'
+    assert pcn((128, 128, 72)).step_form() == 'stream'
+    monkeypatch.setenv('RS_PC_FORM', 'stream:3,8')
+    with pytest.raises(ValueError):
+        pcn((64, 64, 36))
+    monkeypatch.setenv('RS_PC_FORM', 'stream:2,8,3')   # spills at float64: refused
+    with pytest.raises(ValueError):
+        pcn((64, 64, 36), precision='float64')

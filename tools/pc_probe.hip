@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     }
     rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
     unsigned long long* dbg;
-    const size_t ndbg = 2 * 4096 * 8;
+    const size_t ndbg = 5 * 4096 * 8;
     CK(hipMalloc(&dbg, ndbg * 8));
     CK(hipMemset(dbg, 0, ndbg * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
@@ -85,8 +85,10 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
     const int nb = h->nPart;
-    for (int kid = 0; kid < 2; ++kid) {
-        const int ns = kid == 0 ? 4 : (kid == 1 ? 6 : 7);
+    static const char* kname[4] = {"excite_rows", "path_rows", "excite_stream", "path_stream"};
+    static const int kns[4] = {4, 6, 5, 5};
+    for (int kid = 0; kid < 4; ++kid) {
+        const int ns = kns[kid];
         if (st[(size_t)kid * 4096 * 8] == 0) continue;  // kernel not used by this step form
         unsigned long long t0 = ~0ull, t1 = 0;
         std::vector<std::vector<double>> ph(ns);
@@ -100,13 +102,35 @@ int main(int argc, char** argv) {
         std::vector<double> starts;
         for (int b = 0; b < nb; ++b) starts.push_back((st[((size_t)kid * 4096 + b) * 8] - t0) * 10.0);
         printf("%s: first start -> last end %.2f us; start spread median %.2f max %.2f us\n",
-               kid == 0 ? "excite" : (kid == 1 ? "path" : "fused"), (t1 - t0) * 1e-2, median(starts) * 1e-3,
+               kname[kid], (t1 - t0) * 1e-2, median(starts) * 1e-3,
                *std::max_element(starts.begin(), starts.end()) * 1e-3);
         for (int i = 1; i < ns; ++i)
             printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph[i]) * 1e-3,
                    *std::max_element(ph[i].begin(), ph[i].end()) * 1e-3);
     }
-    // back-to-back launch costs
+    if (st[(size_t)4 * 4096 * 8] != 0) {  // shader-clock phases of layer 5 (excite stream)
+        const char* nm[6] = {"vmcnt wait", "lds store+prefetch+barrier", "y pass", "barrier 2",
+                             "x pass", "theta pass"};
+        for (int i = 1; i < 7; ++i) {
+            std::vector<double> c;
+            for (int b = 0; b < h->nPart; ++b) {
+                const unsigned long long* r = &st[((size_t)4 * 4096 + b) * 8];
+                c.push_back((double)(r[i] - r[i - 1]));
+            }
+            printf("   excite layer-5 %-28s median %6.0f cycles\n", nm[i - 1], median(c));
+        }
+    }
+    if (h->streamed) {
+        printf("stream tile BX=%d WR=%d KC=%d grid %d blocks\n", h->sbx, h->swr, h->sg.KC,
+               h->sg.gx * h->sg.gy * h->sg.gz);
+        rs_pc_destroy(h);
+        return 0;
+    }
+    if (Y > 64) {
+        rs_pc_destroy(h);
+        return 0;
+    }
+    // back-to-back launch costs (rows form, Y <= 64)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
