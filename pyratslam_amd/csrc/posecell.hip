@@ -661,8 +661,8 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 }
 
 // ---------------------------------------------------------------------------
-// Layer-streaming forms (the default).  A block of 8 waves owns BXB = BX*WR
-// rows x YT = 64*(8/WR) columns x KC layers of the output and walks its KC + 6
+// Layer-streaming forms (large grids).  A block of WR x WC waves owns BXB = BX*WR
+// rows x YT = 64*WC columns x KC layers of the output and walks its KC + 6
 // input layers in order.  Per input layer only 2-D work is done (window load
 // into double-buffered LDS, then the y and x passes or the 7x7 filter); the
 // 7-tap theta pass runs on a 7-deep register ring of per-lane results, so the
@@ -680,7 +680,6 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 // XCD x takes a contiguous run of tiles, so neighbouring tiles' halo rows and
 // layers meet in the same L2.
 // ---------------------------------------------------------------------------
-constexpr int ST_NT = 512, ST_NW = ST_NT / 64;
 #ifndef PC_ST_PF
 #define PC_ST_PF 3
 #endif
@@ -692,15 +691,16 @@ constexpr int ST_PF = PC_ST_PF;           // window prefetch distance (layers)
 #define PC_ST_WAVES __attribute__((amdgpu_waves_per_eu(1, 2)))
 #endif
 constexpr int ST_MAXKC = 12;              // layers per block (outputs buffered in LDS)
-constexpr int ST_MAXL = ST_MAXKC + 2 * 3 + ST_PF;  // control entries staged in LDS
+constexpr int ST_MAXL = ST_MAXKC + 2 * 3 + ST_PF + 1;  // control entries staged in LDS
 constexpr int ST_OUT_BYTES = 24 * 1024;   // LDS output buffer per block
 // layers per block that fit the output buffer for a tile of bxb x yt cells of esz bytes
 __host__ __device__ constexpr int st_maxkc(int esz, int bxb, int yt) {
     return ST_OUT_BYTES / (esz * bxb * yt) < ST_MAXKC ? ST_OUT_BYTES / (esz * bxb * yt) : ST_MAXKC;
 }
 constexpr int ST_FTP = 52;                // filter stride in LDS: 49 taps padded to 13 x 16 B
-constexpr int NPP_MAX_BLOCKS = 4 * ST_NT * 64;
+constexpr int NPP_MAX_BLOCKS = 4 * 512 * 64;
 constexpr size_t ST_MIN_CELLS = 512 * 1024;  // default form: streamed from this grid size
+constexpr int ST_DEF_BX = 2, ST_DEF_WR = 8, ST_DEF_WC = 1;  // default streaming tile (float32)
 static_assert(ST_PF >= 1 && ST_PF < FL, "prefetch ring has 7 slots");
 
 struct StreamGrid {  // tiles along x, y and theta chunks; layers per chunk
@@ -741,21 +741,20 @@ __device__ inline void st_wait(T (&v)[L]) {
 
 // Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
 // (:339-340) and the normalisation partial sum (:343), streamed over layers.
-template <typename T, int BX, int WR>
-__global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_excite_stream(const T* __restrict__ P, T* __restrict__ Q,
+template <typename T, int BX, int WR, int WC>
+__global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_excite_stream(const T* __restrict__ P, T* __restrict__ Q,
                                                            double* __restrict__ part,
                                                            unsigned long long* __restrict__ res_slot,
                                                            int X, int Y, int TH, StreamGrid G,
                                                            SepKernel<T> k) {
-    constexpr int WC = ST_NW / WR, YT = 64 * WC, BXB = BX * WR;
+    constexpr int NW = WR * WC, NT = 64 * NW, YT = 64 * WC, BXB = BX * WR;
     constexpr int HR = BXB + 2 * HALF, RW = YT + 2 * HALF, WN = HR * RW;
-    constexpr int LPT = (WN + ST_NT - 1) / ST_NT;
-    static_assert(ST_NW % WR == 0, "waves split into WR row groups x WC column tiles");
-    __shared__ T s_in[2][LPT * ST_NT];  // padded: every thread stores every stage
+    constexpr int LPT = (WN + NT - 1) / NT;
+    __shared__ T s_in[2][LPT * NT];  // padded: every thread stores every stage
     __shared__ T s_ye[2][HR * YT];
     __shared__ T s_yi[2][HR * YT];
     __shared__ T s_out[st_maxkc(sizeof(T), BXB, YT) * BXB * YT];
-    __shared__ double s_red[ST_NW];
+    __shared__ double s_red[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rg = wave % WR, col = (wave / WR) * 64 + lane;
     const int tile = st_tile(blockIdx.x, gridDim.x);
@@ -772,7 +771,7 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_excite_stream(const T* _
     unsigned off[LPT];
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-        const int e = min(tid + u * ST_NT, WN - 1), r = e / RW, c = e - r * RW;
+        const int e = min(tid + u * NT, WN - 1), r = e / RW, c = e - r * RW;
         off[u] = (unsigned)(rs::wrapi(i0 - HALF + r, X) * Y + rs::wrapi(y0 - HALF + c, Y));
     }
     const size_t lstride = (size_t)X * Y;
@@ -786,80 +785,92 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_excite_stream(const T* _
 
     T re[FL][BX], ri[FL][BX];
     double sum = 0.0;
+    // software-pipelined over layers, one barrier per iteration: iteration it
+    // stores window it+1, runs the y pass of layer it and the x / theta passes of
+    // layer it-1 (its y pass landed before the previous barrier)
+    st_wait<(ST_PF - 1) * LPT>(pre[0]);
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) s_in[0][tid + u * NT] = pre[0][u];
+    {
+        const T* src = P + (size_t)rs::wrapi(k0 - HALF + ST_PF, TH) * lstride;
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) pre[ST_PF % FL][u] = st_load(src, off[u]);
+    }
+    __syncthreads();
     PC_STAMP(2, 1);
-    for (int base = 0; base < nL; base += FL) {
+    for (int base = 0; base <= nL; base += FL) {
 #pragma unroll
         for (int s = 0; s < FL; ++s) {
             const int it = base + s;
-            if (it >= nL) break;
-            const int b = it & 1;
-            if (it == 5) PC_STAMPC(4, 0);
-            st_wait<(ST_PF - 1) * LPT>(pre[s]);
-            if (it == 5) PC_STAMPC(4, 1);
+            if (it > nL) break;
+            if (it < nL) {
+                const int b = it & 1;
+                // window it+1 (layers past the chunk are valid wrapped addresses: every
+                // load is issued, so the vmcnt count always holds)
+                st_wait<(ST_PF - 1) * LPT>(pre[(s + 1) % FL]);
 #pragma unroll
-            for (int u = 0; u < LPT; ++u) s_in[b][tid + u * ST_NT] = pre[s][u];
-            {  // layers past the chunk are valid (wrapped) addresses: no branch
-                const T* src = P + (size_t)rs::wrapi(k0 - HALF + it + ST_PF, TH) * lstride;
+                for (int u = 0; u < LPT; ++u) s_in[b ^ 1][tid + u * NT] = pre[(s + 1) % FL][u];
+                {
+                    const T* src = P + (size_t)rs::wrapi(k0 - HALF + it + 1 + ST_PF, TH) * lstride;
 #pragma unroll
-                for (int u = 0; u < LPT; ++u) pre[(s + ST_PF) % FL][u] = st_load(src, off[u]);
-            }
-            __syncthreads();
-            if (it == 0) PC_STAMP(2, 2);
-            if (it == 5) PC_STAMPC(4, 2);
-            // y pass: window rows rg, rg + WR, ... (both Gaussians share the loads)
-            for (int r = rg; r < HR; r += WR) {
-                const T* rw = &s_in[b][r * RW + col];
-                T e = 0, g = 0;
-#pragma unroll
-                for (int t = 0; t < FL; ++t) {
-                    const T x = rw[t];
-                    e += k.ge[t] * x;
-                    g += k.gi[t] * x;
+                    for (int u = 0; u < LPT; ++u) pre[(s + 1 + ST_PF) % FL][u] = st_load(src, off[u]);
                 }
-                s_ye[b][r * YT + col] = e;
-                s_yi[b][r * YT + col] = g;
-            }
-            if (it == 5) PC_STAMPC(4, 3);
-            __syncthreads();
-            if (it == 5) PC_STAMPC(4, 4);
-            // x pass: this wave's BX rows, register-blocked over the BX + 6 window rows
-            T ye[BX + 2 * HALF], yi[BX + 2 * HALF];
+                // y pass of layer it: window rows rg, rg + WR, ... (both Gaussians share the loads)
+                for (int r = rg; r < HR; r += WR) {
+                    const T* rw = &s_in[b][r * RW + col];
+                    T e = 0, g = 0;
 #pragma unroll
-            for (int a = 0; a < BX + 2 * HALF; ++a) {
-                ye[a] = s_ye[b][(rg * BX + a) * YT + col];
-                yi[a] = s_yi[b][(rg * BX + a) * YT + col];
-            }
-#pragma unroll
-            for (int i = 0; i < BX; ++i) {
-                T e = 0, g = 0;
-#pragma unroll
-                for (int t = 0; t < FL; ++t) {
-                    e += k.ge[t] * ye[i + t];
-                    g += k.gi[t] * yi[i + t];
+                    for (int t = 0; t < FL; ++t) {
+                        const T x = rw[t];
+                        e += k.ge[t] * x;
+                        g += k.gi[t] * x;
+                    }
+                    s_ye[b][r * YT + col] = e;
+                    s_yi[b][r * YT + col] = g;
                 }
-                re[s][i] = e;
-                ri[s][i] = g;
             }
-            if (it == 5) PC_STAMPC(4, 5);
-            // theta pass over the ring (input it-6+t sits in slot (s+1+t) % 7),
-            // relu(v - inhib), partial sum; the output waits in LDS
-            if (it >= 2 * HALF) {
-                const int o = it - 2 * HALF;
+            if (it >= 1) {
+                // x pass of layer it-1 (ring slot (s+6) % 7): this wave's BX rows,
+                // register-blocked over the BX + 6 window rows
+                const int b = (it - 1) & 1;
+                T ye[BX + 2 * HALF], yi[BX + 2 * HALF];
+#pragma unroll
+                for (int a = 0; a < BX + 2 * HALF; ++a) {
+                    ye[a] = s_ye[b][(rg * BX + a) * YT + col];
+                    yi[a] = s_yi[b][(rg * BX + a) * YT + col];
+                }
 #pragma unroll
                 for (int i = 0; i < BX; ++i) {
                     T e = 0, g = 0;
 #pragma unroll
                     for (int t = 0; t < FL; ++t) {
-                        e += k.ge[t] * re[(s + 1 + t) % FL][i];
-                        g += k.gi[t] * ri[(s + 1 + t) % FL][i];
+                        e += k.ge[t] * ye[i + t];
+                        g += k.gi[t] * yi[i + t];
                     }
-                    const T v = (e - g) * k.scale;
-                    const T q = (v < k.inhib) ? T(0) : v - k.inhib;
-                    s_out[(o * BXB + rg * BX + i) * YT + col] = q;
-                    if (i0 + rg * BX + i < X && gy < Y) sum += (double)q;
+                    re[(s + 6) % FL][i] = e;
+                    ri[(s + 6) % FL][i] = g;
+                }
+                // theta pass for output layer o = it-7 over the ring (input o+t sits in
+                // slot (s+t) % 7), relu(v - inhib), partial sum; the output waits in LDS
+                if (it >= 2 * HALF + 1) {
+                    const int o = it - 2 * HALF - 1;
+#pragma unroll
+                    for (int i = 0; i < BX; ++i) {
+                        T e = 0, g = 0;
+#pragma unroll
+                        for (int t = 0; t < FL; ++t) {
+                            e += k.ge[t] * re[(s + t) % FL][i];
+                            g += k.gi[t] * ri[(s + t) % FL][i];
+                        }
+                        const T v = (e - g) * k.scale;
+                        const T q = (v < k.inhib) ? T(0) : v - k.inhib;
+                        s_out[(o * BXB + rg * BX + i) * YT + col] = q;
+                        if (i0 + rg * BX + i < X && gy < Y) sum += (double)q;
+                    }
                 }
             }
-            if (it == 5) PC_STAMPC(4, 6);
+            __syncthreads();
+            if (it == 0) PC_STAMP(2, 2);
         }
     }
     PC_STAMP(2, 3);
@@ -871,7 +882,7 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_excite_stream(const T* _
             if (gi < X && gy < Y)
                 Q[((size_t)(k0 + o) * X + gi) * Y + gy] = s_out[(o * BXB + rg * BX + i) * YT + col];
         }
-    sum = block_sum_w<ST_NW>(sum, s_red);
+    sum = block_sum_w<NW>(sum, s_red);
     if (tid == 0) part[blockIdx.x] = sum;
     PC_STAMP(2, 4);
 }
@@ -899,23 +910,22 @@ __device__ inline void st_filter(const T* __restrict__ src, T (&f)[FT]) {
 // (:273 -> convolution.py:320-340), clamp (:300), 7-tap theta filter (:310 ->
 // convolution.py:344-359), clamp (:314), normalisation by the excitation total
 // (:343-345, applied at the end), fused argmax (:317-319), streamed over layers.
-template <typename T, int BX, int WR, typename CTL>
-__global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
+template <typename T, int BX, int WR, int WC, typename CTL>
+__global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
     const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
     T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, StreamGrid G) {
-    constexpr int WC = ST_NW / WR, YT = 64 * WC, BXB = BX * WR;
+    constexpr int NW = WR * WC, NT = 64 * NW, YT = 64 * WC, BXB = BX * WR;
     constexpr int HR = BXB + 2 * HALF, RW = YT + 2 * HALF, WN = HR * RW;
-    constexpr int LPT = (WN + ST_NT - 1) / ST_NT;
-    constexpr int NPP = 4;  // normalisation partials per thread (npart <= NPP * ST_NT)
-    static_assert(ST_NW % WR == 0, "waves split into WR row groups x WC column tiles");
-    __shared__ T s_win[2][LPT * ST_NT];  // padded: every thread stores every stage
+    constexpr int LPT = (WN + NT - 1) / NT;
+    constexpr int NPP = 4;  // normalisation partials per thread (npart <= NPP * NT)
+    __shared__ T s_win[2][LPT * NT];  // padded: every thread stores every stage
     __shared__ T s_out[st_maxkc(sizeof(T), BXB, YT) * BXB * YT];
     __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_ox[ST_MAXL], s_oy[ST_MAXL], s_fo[ST_MAXL];
-    __shared__ double s_red[ST_NW];
-    __shared__ T s_bv[ST_NW];
-    __shared__ unsigned s_bl[ST_NW];
+    __shared__ double s_red[NW];
+    __shared__ T s_bv[NW];
+    __shared__ unsigned s_bl[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int rg = wave % WR, col = (wave / WR) * 64 + lane;
     const int tile = st_tile(blockIdx.x, gridDim.x);
@@ -928,24 +938,24 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
 
     // stage the block's control and the filter table; issue the normalisation
     // partials' loads (reduced after the first windows are in flight)
-    if (tid < nL + ST_PF) {  // + the prefetches issued past the chunk
+    if (tid < nL + ST_PF + 1) {  // + the prefetches issued past the chunk
         const int L = rs::wrapi(k0 - HALF + tid, TH);
         s_ox[tid] = rs::wrapi(ctl_ox(ctl, L), X);   // shifts may exceed the grid (vtrans large)
         s_oy[tid] = rs::wrapi(ctl_oy(ctl, L), Y);
         s_fo[tid] = ctl_fi(ctl, L) * ST_FTP;
     }
-    for (int i = tid; i < nf * FT; i += ST_NT) {
+    for (int i = tid; i < nf * FT; i += NT) {
         const int fi = i / FT;
         s_ftab[fi * ST_FTP + (i - fi * FT)] = filt[i];
     }
     double pt[NPP];
 #pragma unroll
     for (int u = 0; u < NPP; ++u) {
-        const int i = tid + u * ST_NT;
+        const int i = tid + u * NT;
         pt[u] = i < npart ? part[i] : 0.0;
     }
     double pextra = 0.0;
-    for (int i = tid + NPP * ST_NT; i < npart; i += ST_NT) pextra += part[i];
+    for (int i = tid + NPP * NT; i < npart; i += NT) pextra += part[i];
     T zf[FL];
 #pragma unroll
     for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
@@ -957,7 +967,7 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
     int er[LPT], ec[LPT];
 #pragma unroll
     for (int u = 0; u < LPT; ++u) {
-        const int e = min(tid + u * ST_NT, WN - 1), r = e / RW;
+        const int e = min(tid + u * NT, WN - 1), r = e / RW;
         er[u] = rs::wrapi(i0 - HALF + r, X);
         ec[u] = rs::wrapi(y0 - HALF + (e - r * RW), Y);
     }
@@ -978,12 +988,19 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
     double tot = pextra;
 #pragma unroll
     for (int u = 0; u < NPP; ++u) tot += pt[u];
-    tot = block_sum_w<ST_NW>(tot, s_red);
+    tot = block_sum_w<NW>(tot, s_red);
     const T tt = (T)tot;
 
     T ring[FL][BX];
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
+    // software-pipelined: iteration it stores window it+1 while filtering window it;
+    // one barrier per iteration
+    st_wait<(ST_PF - 1) * LPT>(pre[0]);
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) s_win[0][tid + u * NT] = pre[0][u];
+    load(ST_PF, pre[ST_PF % FL]);
+    __syncthreads();
     PC_STAMP(3, 1);
     for (int base = 0; base < nL; base += FL) {
 #pragma unroll
@@ -991,11 +1008,12 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
             const int it = base + s;
             if (it >= nL) break;
             const int b = it & 1;
-            st_wait<(ST_PF - 1) * LPT>(pre[s]);
+            // window it+1 (every load is issued, past the chunk too, so the vmcnt
+            // count always holds: see pc_excite_stream)
+            st_wait<(ST_PF - 1) * LPT>(pre[(s + 1) % FL]);
 #pragma unroll
-            for (int u = 0; u < LPT; ++u) s_win[b][tid + u * ST_NT] = pre[s][u];
-            load(it + ST_PF, pre[(s + ST_PF) % FL]);  // straight line: see pc_excite_stream
-            __syncthreads();
+            for (int u = 0; u < LPT; ++u) s_win[b ^ 1][tid + u * NT] = pre[(s + 1) % FL][u];
+            load(it + 1 + ST_PF, pre[(s + 1 + ST_PF) % FL]);
             if (it == 0) PC_STAMP(3, 2);
             T f[FT];
             st_filter<T>(s_ftab + s_fo[it], f);
@@ -1036,6 +1054,7 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
                     }
                 }
             }
+            __syncthreads();
         }
     }
     PC_STAMP(3, 3);
@@ -1062,7 +1081,7 @@ __global__ __launch_bounds__(ST_NT) PC_ST_WAVES void pc_path_stream(
     }
     __syncthreads();
     if (tid == 0) {
-        for (int w = 1; w < ST_NW; ++w)
+        for (int w = 1; w < NW; ++w)
             if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
                 bv = s_bv[w];
                 bl = s_bl[w];
@@ -1268,7 +1287,7 @@ struct rs_pc {
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
-    int sbx = 1, swr = 8;  // streaming tile: BX rows per wave, WR row groups
+    int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
 };
 
@@ -1370,34 +1389,35 @@ PcCtlRing make_ctl_ring(const rs_pc* h, int s) {
                      reinterpret_cast<const double*>(rec + ctl_off_zf(h))};
 }
 
-// Streaming variants instantiated: (BX rows per wave, WR row groups of waves).
-#define PC_STREAM_VARIANTS(X_) X_(1, 8) X_(2, 8) X_(1, 4) X_(2, 4)
+// Streaming variants instantiated: (BX rows per wave, WR row groups, WC column tiles of 64).
+#define PC_STREAM_VARIANTS(X_) X_(1, 8, 1) X_(2, 8, 1) X_(1, 4, 2) X_(2, 4, 2)
 
 template <typename T, typename CTL>
 int pc_launch_stream(rs_pc* h, const T* P, T* Q, unsigned long long* slot, T* bmax, unsigned* bidx,
                      const CTL* ctl, int prof_base) {
     const StreamGrid G = h->sg;
-    const dim3 grid(G.gx * G.gy * G.gz), block(ST_NT);
+    const dim3 grid(G.gx * G.gy * G.gz), block(64 * h->swr * h->swc);
     const SepKernel<T>& k = sep_of<T>(h);
     const T* filt = static_cast<const T*>(h->dFilt);
     bool done = false;
-#define PC_EXCITE_CASE(bx_, wr_)                                                              \
-    if (!done && h->sbx == bx_ && h->swr == wr_) {                                            \
-        hipLaunchKernelGGL((pc_excite_stream<T, bx_, wr_>), grid, block, 0, h->stream, P, Q,   \
+#define PC_EXCITE_CASE(bx_, wr_, wc_)                                                         \
+    if (!done && h->sbx == bx_ && h->swr == wr_ && h->swc == wc_) {                           \
+        hipLaunchKernelGGL((pc_excite_stream<T, bx_, wr_, wc_>), grid, block, 0, h->stream, P, \
+                           Q,                                                                 \
                            h->dPart, slot, h->X, h->Y, h->TH, G, k);                          \
         done = true;                                                                          \
     }
     PC_STREAM_VARIANTS(PC_EXCITE_CASE)
 #undef PC_EXCITE_CASE
-    RS_CHECK(done, RS_ERR_STATE, "no streaming variant BX=%d WR=%d", h->sbx, h->swr);
+    RS_CHECK(done, RS_ERR_STATE, "no streaming variant BX=%d WR=%d WC=%d", h->sbx, h->swr, h->swc);
     RS_HIP(hipGetLastError());
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
     if (!ctl) return RS_OK;
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
     done = false;
-#define PC_PATH_CASE(bx_, wr_)                                                                   \
-    if (!done && h->sbx == bx_ && h->swr == wr_) {                                               \
-        hipLaunchKernelGGL((pc_path_stream<T, bx_, wr_, CTL>), grid, block, 0, h->stream, Q,      \
+#define PC_PATH_CASE(bx_, wr_, wc_)                                                              \
+    if (!done && h->sbx == bx_ && h->swr == wr_ && h->swc == wc_) {                              \
+        hipLaunchKernelGGL((pc_path_stream<T, bx_, wr_, wc_, CTL>), grid, block, 0, h->stream, Q, \
                            static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,  \
                            bmax, bidx, h->X, h->Y, h->TH, G);                                    \
         done = true;                                                                             \
@@ -1582,15 +1602,16 @@ __global__ void pc_scale_kernel(T* __restrict__ P, size_t n, const double* __res
 // which is only sound when the compiler puts no other vector-memory traffic in
 // the layer loop: refuse a variant that spills to scratch.
 template <typename T>
-int pc_stream_scratch(int bx, int wr, size_t* bytes) {
+int pc_stream_scratch(int bx, int wr, int wc, size_t* bytes) {
     hipFuncAttributes a{};
     *bytes = 0;
     bool done = false;
-#define PC_SCRATCH(bx_, wr_)                                                                 \
-    if (!done && bx == bx_ && wr == wr_) {                                                   \
-        const void* fns[3] = {reinterpret_cast<const void*>(&pc_excite_stream<T, bx_, wr_>), \
-                              reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, PcCtlRing>), \
-                              reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, PcCtlInline>)}; \
+#define PC_SCRATCH(bx_, wr_, wc_)                                                                      \
+    if (!done && bx == bx_ && wr == wr_ && wc == wc_) {                                                \
+        const void* fns[3] = {                                                                         \
+            reinterpret_cast<const void*>(&pc_excite_stream<T, bx_, wr_, wc_>),                        \
+            reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, wc_, PcCtlRing>),               \
+            reinterpret_cast<const void*>(&pc_path_stream<T, bx_, wr_, wc_, PcCtlInline>)};            \
         for (const void* f : fns) {                                                          \
             RS_HIP(hipFuncGetAttributes(&a, f));                                             \
             *bytes += a.localSizeBytes;                                                      \
@@ -1603,7 +1624,7 @@ int pc_stream_scratch(int bx, int wr, size_t* bytes) {
 }
 
 int pc_choose_form(rs_pc* h) {
-    int bx = 1, wr = 8, kc = 0;
+    int bx = 1, wr = 8, wc = 1, kc = 0;
     const char* env = std::getenv("RS_PC_FORM");
     if (env && std::strcmp(env, "rows") == 0) {
         RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=rows needs Y <= 128");
@@ -1615,22 +1636,25 @@ int pc_choose_form(rs_pc* h) {
         h->tiling = 0;
         return RS_OK;
     }
-    if (env && std::strncmp(env, "stream:", 7) == 0) {
-        const int n = std::sscanf(env + 7, "%d,%d,%d", &bx, &wr, &kc);
-        RS_CHECK(n >= 2, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR[,KC], got '%s'", env);
+    const bool explicit_stream = env && std::strncmp(env, "stream:", 7) == 0;
+    if (explicit_stream) {
+        const int n = std::sscanf(env + 7, "%d,%d,%d,%d", &bx, &wr, &wc, &kc);
+        RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR[,KC]])", env);
+                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
-        // (128x128x72: 57 us rows vs 42 us streamed, bx 2)
+        // (128x128x72: 57 us rows vs 41 us streamed)
         const bool big = (size_t)h->X * h->Y * h->TH >= ST_MIN_CELLS;
         if ((env == nullptr || env[0] == 0) && h->tiling != 0 && !big) {
             h->streamed = false;
             return RS_OK;
         }
-        bx = h->esz == 4 ? 2 : 1;
+        bx = h->esz == 4 ? ST_DEF_BX : 1;
+        wr = ST_DEF_WR;
+        wc = ST_DEF_WC;
     }
     if (h->nf > RT_NFMAX) {  // filter table too large to stage in LDS: rows / tiles forms
         RS_CHECK(env == nullptr || std::strncmp(env, "stream", 6) != 0, RS_ERR_ARG,
@@ -1638,32 +1662,32 @@ int pc_choose_form(rs_pc* h) {
         h->streamed = false;
         return RS_OK;
     }
-    const int bxb = bx * wr, yt = 64 * (ST_NW / (wr > 0 ? wr : 1));
+    bool known = false;
+#define PC_KNOWN(bx_, wr_, wc_) known = known || (bx == bx_ && wr == wr_ && wc == wc_);
+    PC_STREAM_VARIANTS(PC_KNOWN)
+#undef PC_KNOWN
+    RS_CHECK(known, RS_ERR_ARG, "no streaming variant BX=%d WR=%d WC=%d", bx, wr, wc);
+    size_t scratch = 0;
+    if (h->esz == 4)
+        RS_TRY(pc_stream_scratch<float>(bx, wr, wc, &scratch));
+    else
+        RS_TRY(pc_stream_scratch<double>(bx, wr, wc, &scratch));
+    RS_CHECK(scratch == 0, RS_ERR_ARG,
+             "streaming variant BX=%d WR=%d WC=%d spills %zu B to scratch at this precision", bx, wr,
+             wc, scratch);
+    const int bxb = bx * wr, yt = 64 * wc;
     StreamGrid g;
     g.gx = (h->X + bxb - 1) / bxb;
     g.gy = (h->Y + yt - 1) / yt;
-    bool known = false;
-#define PC_KNOWN(bx_, wr_) known = known || (bx == bx_ && wr == wr_);
-    PC_STREAM_VARIANTS(PC_KNOWN)
-#undef PC_KNOWN
-    RS_CHECK(known, RS_ERR_ARG, "no streaming variant BX=%d WR=%d", bx, wr);
-    size_t scratch = 0;
-    if (h->esz == 4)
-        RS_TRY(pc_stream_scratch<float>(bx, wr, &scratch));
-    else
-        RS_TRY(pc_stream_scratch<double>(bx, wr, &scratch));
-    RS_CHECK(scratch == 0, RS_ERR_ARG,
-             "streaming variant BX=%d WR=%d spills %zu B to scratch at this precision", bx, wr,
-             scratch);
+    const int maxkc = st_maxkc((int)h->esz, bxb, yt);
     if (kc <= 0) {
-        // smallest chunk that keeps the grid within one block per CU (fewer, longer
-        // blocks re-evaluate fewer halo layers)
+        // smallest chunk that keeps the grid within one block per CU: a second block
+        // on some CUs doubles their share (fewer, longer blocks also re-evaluate
+        // fewer halo layers)
         const int target = 256;
         kc = 2;
-        while (kc < ST_MAXKC && kc < h->TH && (long)g.gx * g.gy * ((h->TH + kc - 1) / kc) > target) ++kc;
+        while (kc < maxkc && kc < h->TH && (long)g.gx * g.gy * ((h->TH + kc - 1) / kc) > target) ++kc;
     }
-    const int maxkc = st_maxkc((int)h->esz, bxb, yt);
-    if (kc > maxkc && (env == nullptr || std::strncmp(env, "stream:", 7) != 0)) kc = maxkc;
     RS_CHECK(kc >= 1 && kc <= maxkc, RS_ERR_ARG, "stream KC=%d outside [1, %d]", kc, maxkc);
     if (kc > h->TH) kc = h->TH;
     g.KC = kc;
@@ -1673,6 +1697,7 @@ int pc_choose_form(rs_pc* h) {
     h->streamed = true;
     h->sbx = bx;
     h->swr = wr;
+    h->swc = wc;
     h->sg = g;
     return RS_OK;
 }

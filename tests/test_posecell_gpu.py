@@ -191,9 +191,9 @@ def test_simulate_driver(pcn):
 # tiled single-pass forms and the layer-streaming form at several tile shapes
 # (rows per wave, row groups, layers per block), incl. ragged tiles and grids
 # whose theta extent is not a multiple of the chunk
-FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,2', 'stream:1,8,5', 'stream:2,8,3',
-                     'stream:1,4,3', 'stream:2,4,6'],
-         'float64': ['rows', 'tiles', 'stream:1,8,2', 'stream:1,8,5', 'stream:1,4,3']}
+FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
+                     'stream:1,4,2,3', 'stream:2,4,2,6'],
+         'float64': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
@@ -220,9 +220,9 @@ def test_default_form_by_grid_size(pcn, monkeypatch):
     monkeypatch.delenv('RS_PC_FORM', raising=False)
     assert pcn((64, 64, 36)).step_form() == 'rows'
     assert pcn((128, 128, 72)).step_form() == 'stream'
-    monkeypatch.setenv('RS_PC_FORM', 'stream:3,8')
+    monkeypatch.setenv('RS_PC_FORM', 'stream:3,8,1')
     with pytest.raises(ValueError):
         pcn((64, 64, 36))
-    monkeypatch.setenv('RS_PC_FORM', 'stream:2,8,3')   # spills at float64: refused
+    monkeypatch.setenv('RS_PC_FORM', 'stream:2,8,1,3')   # spills at float64: refused
     with pytest.raises(ValueError):
         pcn((64, 64, 36), precision='float64')
