@@ -28,6 +28,8 @@
  *   rs_vt_match_batch  a loop of ViewTemplates.match calls (exact sequential
  *                   semantics incl. in-batch appends), or a frozen-library scan
  *   rs_vt_read      ViewTemplate.template         view_templates.py:11
+ *   rs_vt_set_subsample / rs_vt_match_frames
+ *                   input[self.mask].reshape(...) view_templates.py:48-57,64 (on device)
  *   rs_comm_*, rs_vt_attach_comm  (new) RCCL sharding of the library over GPUs
  */
 #ifndef RATSLAM_ABI_H
@@ -152,6 +154,14 @@ int rs_vt_match_batch(rs_vt* h, int nq, const uint8_t* queries, int mode,
 /* single query, RS_VT_SEQUENTIAL semantics */
 int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* best_index,
                 int* is_new);
+/* On-device subsampling (view_templates.py:64, input[self.mask].reshape(shape)):
+ * pixels[H*W] are the byte offsets, in a frame of frame_bytes, of the pixels the
+ * mask keeps, in template row-major order (view_templates.py:48-57).  Then
+ * rs_vt_match_frames matches nf whole frames (frame_bytes each; host memory, or
+ * device memory the GPU gathers from in place) with rs_vt_match_batch semantics. */
+int rs_vt_set_subsample(rs_vt* h, int64_t frame_bytes, const int32_t* pixels);
+int rs_vt_match_frames(rs_vt* h, int nf, const uint8_t* frames, int mode, uint64_t* best_score,
+                       int64_t* best_index, uint8_t* is_new);
 /* all pair scores of nq queries vs templates [t0, t0+nt) (owning rank's slots only;
  * nranks must be 1): scores[q*nt + t]  -- ViewTemplate.match per pair */
 int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t nt,

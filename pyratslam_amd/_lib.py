@@ -80,6 +80,8 @@ SIGNATURES = {
     'rs_vt_match_batch': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int, _u64p, _i64p, _u8p]),
     'rs_vt_match': (ctypes.c_int, [_vp, _u8p, _u64p, _i64p, _c_int_p]),
     'rs_vt_scores': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int64, ctypes.c_int64, _u64p]),
+    'rs_vt_set_subsample': (ctypes.c_int, [_vp, ctypes.c_int64, _i32p]),
+    'rs_vt_match_frames': (ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_int, _u64p, _i64p, _u8p]),
     'rs_vt_scan_local': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, _u64p]),
     'rs_vt_resolve': (ctypes.c_int, [_vp, ctypes.c_int, _u64p, ctypes.c_int, _u64p, _i64p, _u8p]),
     'rs_vt_last_ms': (ctypes.c_int, [_vp, _f64p]),

@@ -25,6 +25,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -79,6 +80,17 @@ __global__ void vt_store_kernel(const uint8_t* __restrict__ raw, const int32_t* 
         const int64_t tb = slot >> 6, tl = slot & 63;
         lib[((tb * WD + c) * HQ + q) * 64 + tl] = make_uint4(w[0], w[1], w[2], w[3]);
     }
+}
+
+// On-device subsampling (view_templates.py:64, input[self.mask].reshape(shape)):
+// query f = frame f gathered through the mask's pixel offsets, row-major.
+__global__ __launch_bounds__(256) void vt_gather_kernel(const uint8_t* __restrict__ frames,
+                                                        size_t frame_bytes,
+                                                        const int32_t* __restrict__ pix, int npix,
+                                                        uint8_t* __restrict__ out) {
+    const uint8_t* f = frames + (size_t)blockIdx.x * frame_bytes;
+    uint8_t* o = out + (size_t)blockIdx.x * npix;
+    for (int i = threadIdx.x; i < npix; i += blockDim.x) o[i] = f[pix[i]];
 }
 
 // Query forms: qf[(n*WD + c)*H + r] = (cL, cH) of c = -Q[r][4c..4c+3] mod 256,
@@ -871,6 +883,12 @@ struct rs_vt {
     int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
     unsigned* dCtr = nullptr;  // per template block x query group: next batch (plane scan)
     int ctrCap = 0;
+    // on-device subsampling of camera frames (rs_vt_set_subsample / rs_vt_match_frames)
+    int32_t* dPix = nullptr;   // H*W byte offsets of the kept pixels in a frame
+    int64_t frameBytes = 0;
+    uint8_t* dFrames = nullptr;
+    uint8_t* hFrames = nullptr;  // pinned staging for host frames
+    int frameCap = 0;
 };
 
 namespace {
@@ -1006,12 +1024,19 @@ int vt_grow_cand(rs_vt* h, int64_t slots) {
     return RS_OK;
 }
 
+int vt_build_forms(rs_vt* h, int nq);
+
 // Upload nq raw queries and build their forms on the device.
 int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     RS_TRY(vt_grow_queries(h, nq));
     const size_t qb = (size_t)h->H * h->W * nq;
     std::memcpy(h->hQraw, queries, qb);
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    return vt_build_forms(h, nq);
+}
+
+// Build the query forms of the nq raw queries already in dQraw.
+int vt_build_forms(rs_vt* h, int nq) {
     hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H, h->W,
                        h->WD, h->M, h->dQf, h->dQsum);
     if (h->planar)
@@ -1019,6 +1044,40 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
                            h->M, h->dQp, h->dQsumRaw);
     RS_HIP(hipGetLastError());
     return RS_OK;
+}
+
+// Subsample nf frames on the device into the raw query buffer, then build the
+// forms.  Host frames go through a pinned staging buffer; device-resident frames
+// (a camera / decoder pipeline on the GPU) are gathered in place.
+int vt_stage_frames(rs_vt* h, int nf, const uint8_t* frames) {
+    RS_CHECK(h->dPix, RS_ERR_STATE, "no subsampling mask: call rs_vt_set_subsample first");
+    RS_TRY(vt_grow_queries(h, nf));
+    hipPointerAttribute_t attr{};
+    const bool on_device = hipPointerGetAttributes(&attr, frames) == hipSuccess &&
+                           attr.type == hipMemoryTypeDevice;
+    (void)hipGetLastError();  // a host pointer is not an error
+    const uint8_t* src = frames;
+    if (!on_device) {
+        if (nf > h->frameCap) {
+            int cap = h->frameCap > 0 ? h->frameCap : 16;
+            while (cap < nf) cap *= 2;
+            if (h->dFrames) RS_HIP(hipFree(h->dFrames));
+            if (h->hFrames) RS_HIP(hipHostFree(h->hFrames));
+            h->dFrames = nullptr;
+            h->hFrames = nullptr;
+            RS_HIP(hipMalloc(&h->dFrames, (size_t)h->frameBytes * cap));
+            RS_HIP(hipHostMalloc(&h->hFrames, (size_t)h->frameBytes * cap, hipHostMallocDefault));
+            h->frameCap = cap;
+        }
+        const size_t fb = (size_t)h->frameBytes * nf;
+        std::memcpy(h->hFrames, frames, fb);
+        RS_HIP(hipMemcpyAsync(h->dFrames, h->hFrames, fb, hipMemcpyHostToDevice, h->stream));
+        src = h->dFrames;
+    }
+    hipLaunchKernelGGL(vt_gather_kernel, dim3(nf), dim3(256), 0, h->stream, src,
+                       (size_t)h->frameBytes, h->dPix, h->H * h->W, h->dQraw);
+    RS_HIP(hipGetLastError());
+    return vt_build_forms(h, nf);
 }
 
 // Store raw staged queries src[i] into slots dst[i] of the library (or, with
@@ -1157,13 +1216,17 @@ int vt_append_staged(rs_vt* h, const std::vector<std::pair<int, int64_t>>& news)
     return RS_OK;
 }
 
-// Stage nq queries and min-reduce their local first-argmin keys into dBest.
-int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries) {
+// Stage nq queries (raw H x W, or whole frames subsampled on the device) and
+// min-reduce their local first-argmin keys into dBest.
+int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = false) {
     RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
     RS_CHECK(nq >= 0, RS_ERR_ARG, "negative query count");
     if (nq == 0) return RS_OK;
     RS_HIP(hipSetDevice(h->device));
-    if (queries) {
+    if (frames) {
+        RS_CHECK(queries, RS_ERR_ARG, "null frames");
+        RS_TRY(vt_stage_frames(h, nq, queries));
+    } else if (queries) {
         RS_TRY(vt_stage_queries(h, nq, queries));
     } else {
         // re-match the queries already resident on the device (last staged batch)
@@ -1269,9 +1332,9 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
 }
 
 int vt_match_impl(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64_t* best_score,
-                  int64_t* best_index, uint8_t* is_new) {
+                  int64_t* best_index, uint8_t* is_new, bool frames = false) {
     RS_CHECK(mode == RS_VT_FROZEN || mode == RS_VT_SEQUENTIAL, RS_ERR_ARG, "unknown mode %d", mode);
-    RS_TRY(vt_scan_local_impl(h, nq, queries));
+    RS_TRY(vt_scan_local_impl(h, nq, queries, frames));
     if (nq == 0) return RS_OK;
     RS_TRY(vt_fetch_keys(h, nq, true));
     return vt_resolve_impl(h, nq, h->hBest, mode, best_score, best_index, is_new);
@@ -1359,9 +1422,10 @@ int rs_vt_destroy(rs_vt* h) {
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
                     (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
-                    (void*)h->dQsumRaw, (void*)h->dCtr})
+                    (void*)h->dQsumRaw, (void*)h->dCtr, (void*)h->dPix, (void*)h->dFrames})
         if (p) (void)hipFree(p);
-    for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat})
+    for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat,
+                    (void*)h->hFrames})
         if (p) (void)hipHostFree(p);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -1435,6 +1499,38 @@ int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* b
     const int s = vt_match_impl(h, 1, query, RS_VT_SEQUENTIAL, best_score, best_index, &nw);
     if (is_new) *is_new = nw;
     return s;
+}
+
+int rs_vt_set_subsample(rs_vt* h, int64_t frame_bytes, const int32_t* pixels) {
+    rs::clear_error();
+    RS_CHECK(h && pixels, RS_ERR_ARG, "null argument");
+    RS_CHECK(frame_bytes > 0 && frame_bytes <= INT32_MAX, RS_ERR_ARG, "bad frame size %lld",
+             (long long)frame_bytes);
+    const int npix = h->H * h->W;
+    for (int i = 0; i < npix; ++i)
+        RS_CHECK(pixels[i] >= 0 && pixels[i] < frame_bytes, RS_ERR_ARG,
+                 "pixel offset %d of entry %d outside the %lld-byte frame", pixels[i], i,
+                 (long long)frame_bytes);
+    RS_HIP(hipSetDevice(h->device));
+    if (!h->dPix) RS_HIP(hipMalloc(&h->dPix, sizeof(int32_t) * npix));
+    RS_HIP(hipMemcpyAsync(h->dPix, pixels, sizeof(int32_t) * npix, hipMemcpyHostToDevice, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    if (frame_bytes != h->frameBytes) {  // staging buffers are sized per frame
+        if (h->dFrames) RS_HIP(hipFree(h->dFrames));
+        if (h->hFrames) RS_HIP(hipHostFree(h->hFrames));
+        h->dFrames = nullptr;
+        h->hFrames = nullptr;
+        h->frameCap = 0;
+    }
+    h->frameBytes = frame_bytes;
+    return RS_OK;
+}
+
+int rs_vt_match_frames(rs_vt* h, int nf, const uint8_t* frames, int mode, uint64_t* best_score,
+                       int64_t* best_index, uint8_t* is_new) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    return vt_match_impl(h, nf, frames, mode, best_score, best_index, is_new, true);
 }
 
 int rs_vt_scan_local(rs_vt* h, int nq, const uint8_t* queries, uint64_t* local_keys) {

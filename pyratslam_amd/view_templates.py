@@ -201,6 +201,73 @@ class ViewTemplates:
         idx, _, _ = self.match_templates(q, pcs)
         return [self.templates[int(i)] for i in idx]
 
+    # -- on-device subsampling --------------------------------------------------
+    def _ensure_gather(self):
+        if getattr(self, '_gather_ready', False):
+            return
+        if self.mask is None:
+            raise ValueError('no subsampling mask: construct with the frame geometry')
+        pix = np.ascontiguousarray(np.flatnonzero(self.mask.ravel()), dtype=np.int32)
+        assert pix.size == self.shape[0] * self.shape[1]
+        _lib.check(self._lib.rs_vt_set_subsample(self._h, self.mask.size,
+                                                 _lib.ptr(pix, ctypes.c_int32)))
+        self._gather_ready = True
+
+    def match_frames(self, frames, pcs, mode=_lib.RS_VT_SEQUENTIAL):
+        """``match`` for a batch of whole frames, subsampled on the GPU
+        (view_templates.py:64 as a device gather through the mask's pixel offsets).
+
+        ``frames``: uint8 (n, im_x, im_y) host array, or a device-resident uint8
+        tensor of that shape (anything with ``data_ptr()``/``is_cuda``, e.g. a
+        torch CUDA tensor), gathered in place.  Returns ``(index, score, is_new)``
+        like ``match_templates``.
+        """
+        self._ensure_gather()
+        dev = getattr(frames, 'is_cuda', False)
+        if dev:
+            n = int(frames.shape[0])
+            if str(frames.dtype) != 'torch.uint8' or tuple(frames.shape[1:]) != self.mask.shape \
+                    or not frames.is_contiguous():
+                raise TypeError('device frames must be a contiguous uint8 (n, %d, %d) tensor'
+                                % self.mask.shape)
+            fptr = ctypes.c_void_p(frames.data_ptr())
+        else:
+            f = np.asarray(frames)
+            if f.dtype != np.uint8:
+                raise TypeError('ViewTemplates matches uint8 frames (mono8, ros_simulate.py:100-101); '
+                                'got %s' % f.dtype)
+            if f.shape[1:] != self.mask.shape:
+                raise ValueError('frame shape %r does not match the mask %r' % (f.shape[1:], self.mask.shape))
+            f = np.ascontiguousarray(f)
+            n = f.shape[0]
+            fptr = ctypes.c_void_p(f.ctypes.data)
+        idx = np.empty(n, dtype=np.int64)
+        score = np.empty(n, dtype=np.uint64)
+        new = np.zeros(n, dtype=np.uint8)
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_match_frames(self._h, n, fptr, mode,
+                                                    _lib.ptr(score, ctypes.c_uint64),
+                                                    _lib.ptr(idx, ctypes.c_int64),
+                                                    _lib.ptr(new, ctypes.c_uint8)))
+            if mode == _lib.RS_VT_SEQUENTIAL:
+                pcs = pcs if pcs is not None else [(0, 0, 0)] * n
+                for i in range(n):
+                    if new[i]:
+                        if dev:
+                            t = np.empty(self.shape, dtype=np.uint8)
+                            if self.nranks == 1:
+                                _lib.check(self._lib.rs_vt_read(self._h, int(idx[i]),
+                                                                _lib.ptr(t, ctypes.c_uint8)))
+                            else:  # bytes live on the owning rank only
+                                t = frames[i].cpu().numpy()[self.mask].reshape(self.shape)
+                        else:
+                            t = f[i][self.mask].reshape(self.shape)
+                        p = pcs[i]
+                        assert idx[i] == len(self.templates), (idx[i], len(self.templates))
+                        self.templates.append(ViewTemplate(p[0], p[1], p[2], int(idx[i]), t,
+                                                           _owner=self))
+        return idx, score, new.astype(bool)
+
     def device_ms(self):
         ms = ctypes.c_double()
         _lib.check(self._lib.rs_vt_last_ms(self._h, ctypes.byref(ms)))

@@ -226,3 +226,61 @@ def test_library_growth(vtmod):
         lib.add(data[lo:lo + 100])
     idx, score, _ = lib.match_templates(data[::37], mode=0)
     assert np.array_equal(idx, np.arange(0, 700, 37)) and (score == 0).all()
+
+
+def noisy_frame(mask, template, rng):
+    """A frame whose masked pixels carry the template and every other pixel noise,
+    so only a gather through exactly the mask's offsets reproduces the template."""
+    im = rng.integers(0, 256, mask.shape, dtype=np.uint8)
+    im[mask] = template.ravel()
+    return im
+
+
+@pytest.mark.parametrize('name', ['vt_trace_ros', 'vt_trace_64x32'])
+def test_trace_via_match_frames(vtmod, name):
+    """On-device subsampling (view_templates.py:64 as a GPU gather) + matching of
+    whole frames reproduces the reference's library-evolution trace."""
+    d = load_golden(name)
+    p = [int(v) for v in d['params']]
+    vts = vtmod.ViewTemplates((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    rng = np.random.default_rng(5)
+    frames = np.stack([noisy_frame(vts.mask, q, rng) for q in d['queries']])
+    third = len(frames) // 3
+    got = []
+    for lo, hi in ((0, third), (third, 2 * third), (2 * third, len(frames))):
+        idx, _, _ = vts.match_frames(frames[lo:hi], d['pcs'][lo:hi])
+        got.append(idx)
+    assert np.array_equal(np.concatenate(got), d['index'])
+    assert np.array_equal(np.stack([t.template for t in vts.templates]), d['templates'])
+    assert np.array_equal(np.array([t.location() for t in vts.templates]), d['locations'])
+
+
+def test_match_frames_device_resident(vtmod):
+    """Frames already in HBM (a torch CUDA tensor) are gathered in place and give
+    the same answers as host frames."""
+    torch = pytest.importorskip('torch')
+    if not torch.cuda.is_available():
+        pytest.skip('no HIP device for torch')
+    d = load_golden('vt_trace_ros')
+    p = [int(v) for v in d['params']]
+    a = vtmod.ViewTemplates((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    b = vtmod.ViewTemplates((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7], p[8])
+    rng = np.random.default_rng(6)
+    frames = np.stack([noisy_frame(a.mask, q, rng) for q in d['queries'][:120]])
+    ia, sa, na = a.match_frames(frames, d['pcs'][:120])
+    ib, sb, nb = b.match_frames(torch.from_numpy(frames).to('cuda:0'), d['pcs'][:120])
+    assert np.array_equal(ia, ib) and np.array_equal(sa, sb) and np.array_equal(na, nb)
+    assert np.array_equal(ia, d['index'][:120])
+    assert np.array_equal(np.stack([t.template for t in b.templates]),
+                          np.stack([t.template for t in a.templates]))
+
+
+def test_match_frames_errors(vtmod):
+    vts = vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, 45000)
+    with pytest.raises(TypeError):
+        vts.match_frames(np.zeros((2, 256, 256), dtype=np.float32), None)
+    with pytest.raises(ValueError):
+        vts.match_frames(np.zeros((2, 128, 256), dtype=np.uint8), None)
+    lone = vtmod.ViewTemplates._from_shape((32, 32), 45000)
+    with pytest.raises(ValueError):
+        lone.match_frames(np.zeros((1, 256, 256), dtype=np.uint8), None)
