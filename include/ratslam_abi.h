@@ -63,6 +63,11 @@ int rs_version(void);
 const char* rs_last_error(void);
 /* number of visible HIP devices (0 if none / no driver) */
 int rs_device_count(void);
+/* device buffers for callers that keep inputs resident in HBM without a framework
+ * (e.g. camera frames for rs_vt_match_frames); rs_dev_copy copies in any direction */
+int rs_dev_malloc(int device, size_t bytes, void** ptr);
+int rs_dev_free(void* ptr);
+int rs_dev_copy(void* dst, const void* src, size_t bytes);
 
 /* ------------------------------------------------------------------------ */
 /* Pose-cell network                                                         */

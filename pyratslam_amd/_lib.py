@@ -55,6 +55,9 @@ SIGNATURES = {
     'rs_version': (ctypes.c_int, []),
     'rs_last_error': (ctypes.c_char_p, []),
     'rs_device_count': (ctypes.c_int, []),
+    'rs_dev_malloc': (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    'rs_dev_free': (ctypes.c_int, [_vp]),
+    'rs_dev_copy': (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     'rs_pc_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(PcParams), ctypes.c_int, ctypes.POINTER(_vp)]),
     'rs_pc_destroy': (ctypes.c_int, [_vp]),
@@ -154,3 +157,33 @@ def ptr(a, ctype):
 
 def as_c(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
+
+
+class DeviceBuffer:
+    """A block of HBM owned by the caller (rs_dev_malloc); ``ptr`` is the device
+    address, usable wherever the C ABI accepts device-resident inputs."""
+
+    def __init__(self, nbytes, device=0):
+        self._lib = require_device()
+        p = ctypes.c_void_p()
+        check(self._lib.rs_dev_malloc(int(device), int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p, int(nbytes)
+
+    def upload(self, array):
+        import numpy as np
+        a = np.ascontiguousarray(array)
+        if a.nbytes > self.nbytes:
+            raise ValueError('%d bytes do not fit a %d-byte buffer' % (a.nbytes, self.nbytes))
+        check(self._lib.rs_dev_copy(self.ptr, ctypes.c_void_p(a.ctypes.data), a.nbytes))
+        return self
+
+    def close(self):
+        if getattr(self, 'ptr', None) is not None and self.ptr.value:
+            self._lib.rs_dev_free(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -30,4 +30,26 @@ int rs_device_count(void) {
     return n;
 }
 
+int rs_dev_malloc(int device, size_t bytes, void** ptr) {
+    rs::clear_error();
+    RS_CHECK(ptr, RS_ERR_ARG, "null output pointer");
+    *ptr = nullptr;
+    RS_HIP(hipSetDevice(device));
+    RS_HIP(hipMalloc(ptr, bytes));
+    return RS_OK;
+}
+
+int rs_dev_free(void* ptr) {
+    rs::clear_error();
+    if (ptr) RS_HIP(hipFree(ptr));
+    return RS_OK;
+}
+
+int rs_dev_copy(void* dst, const void* src, size_t bytes) {
+    rs::clear_error();
+    RS_CHECK(dst && src, RS_ERR_ARG, "null pointer");
+    RS_HIP(hipMemcpy(dst, src, bytes, hipMemcpyDefault));
+    return RS_OK;
+}
+
 }  // extern "C"

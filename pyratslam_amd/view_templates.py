@@ -217,20 +217,18 @@ class ViewTemplates:
         """``match`` for a batch of whole frames, subsampled on the GPU
         (view_templates.py:64 as a device gather through the mask's pixel offsets).
 
-        ``frames``: uint8 (n, im_x, im_y) host array, or a device-resident uint8
-        tensor of that shape (anything with ``data_ptr()``/``is_cuda``, e.g. a
-        torch CUDA tensor), gathered in place.  Returns ``(index, score, is_new)``
-        like ``match_templates``.
+        ``frames``: uint8 (n, im_x, im_y) host array, or frames already in HBM as
+        ``(n, _lib.DeviceBuffer)`` (n whole frames back to back), gathered in
+        place.  Returns ``(index, score, is_new)`` like ``match_templates``.
         """
         self._ensure_gather()
-        dev = getattr(frames, 'is_cuda', False)
+        dev = isinstance(frames, tuple)
         if dev:
-            n = int(frames.shape[0])
-            if str(frames.dtype) != 'torch.uint8' or tuple(frames.shape[1:]) != self.mask.shape \
-                    or not frames.is_contiguous():
-                raise TypeError('device frames must be a contiguous uint8 (n, %d, %d) tensor'
-                                % self.mask.shape)
-            fptr = ctypes.c_void_p(frames.data_ptr())
+            n, buf = int(frames[0]), frames[1]
+            if n * self.mask.size > buf.nbytes:
+                raise ValueError('%d frames of %d bytes exceed the %d-byte device buffer'
+                                 % (n, self.mask.size, buf.nbytes))
+            fptr = buf.ptr
         else:
             f = np.asarray(frames)
             if f.dtype != np.uint8:
@@ -253,13 +251,13 @@ class ViewTemplates:
                 pcs = pcs if pcs is not None else [(0, 0, 0)] * n
                 for i in range(n):
                     if new[i]:
-                        if dev:
+                        if dev:  # the gathered bytes: read back from the owning rank
                             t = np.empty(self.shape, dtype=np.uint8)
-                            if self.nranks == 1:
+                            if int(idx[i]) % self.nranks == self.rank:
                                 _lib.check(self._lib.rs_vt_read(self._h, int(idx[i]),
                                                                 _lib.ptr(t, ctypes.c_uint8)))
-                            else:  # bytes live on the owning rank only
-                                t = frames[i].cpu().numpy()[self.mask].reshape(self.shape)
+                            else:
+                                t = None
                         else:
                             t = f[i][self.mask].reshape(self.shape)
                         p = pcs[i]
