@@ -108,6 +108,8 @@ int rs_pc_run(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32
 /* steps 1-4 of update() alone (excitation, global inhibition, normalisation):
  * the state the reference leaves behind when path_integration raises KeyError */
 int rs_pc_excite(rs_pc* h);
+/* posecells[x][y][th] += energy; queued on the handle's stream (returns without a
+ * host sync), ordered before the next update / read / argmax */
 int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th);
 int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]);
 /* whole volume as float64, C order (X, Y, TH) -- the reference's .posecells */

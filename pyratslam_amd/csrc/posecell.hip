@@ -1865,7 +1865,8 @@ int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th) {
         hipLaunchKernelGGL((pc_inject_kernel<double>), dim3(1), dim3(64), 0, h->stream,
                            static_cast<double*>(h->dP), idx, energy);
     RS_HIP(hipGetLastError());
-    RS_HIP(hipStreamSynchronize(h->stream));
+    // no host sync: the add is ordered on the handle's stream before the next step,
+    // read or argmax (template -> pose-cell feedback costs one queued launch)
     return RS_OK;
 }
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate golden vectors by running the REFERENCE itself (build container only).
 
-Runs ``/root/reference/ratslam/{posecell_network,convolution,view_templates}.py``
+Runs ``/root/reference/ratslam/{posecell_network,convolution,view_templates,experience_map}.py``
 under Python 3 with the minimum shims needed to reproduce their Python-2
 behaviour, and with the reference's own OpenCL kernel text (rendered by its own
 ``Convolution.set_text``) compiled as host C by gcc (``-ffp-contract=off``) in
@@ -372,14 +372,48 @@ def gen_templates(vt, out):
     trace('vt_trace_64x32', 160, (16, 144), (16, 80), 2, 45000, 300, 6, 3)
 
 
+def gen_ros_replay(pn, vt, out, n=120, seed=0):
+    """Config 5 end to end with the reference's own classes: PoseCellNetwork,
+    ViewTemplates and ExperienceMap (experience_map.py, imported unmodified)
+    driven through RatslamRos's callback logic (ros_simulate.py:98-162, restated
+    in pyratslam_amd.replay because rospy/cv are absent) over the synthetic
+    stand-in for the absent dataset_10Hz.bag (pyratslam_amd.synthetic.ros_stream)."""
+    import experience_map as em_ref   # noqa: E402  (REF is on sys.path)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, root)
+    from pyratslam_amd import replay, synthetic
+    pcn = pn.PoseCellNetwork(replay.POSE_SIZE)
+    vts = vt.ViewTemplates(x_range=replay.X_RANGE, y_range=replay.Y_RANGE, x_step=Py2Int(replay.X_STEP),
+                           y_step=Py2Int(replay.Y_STEP), im_x=replay.IM_SIZE[0], im_y=replay.IM_SIZE[1],
+                           match_threshold=replay.MATCH_THRESHOLD)
+    vts.shape = tuple(int(s) for s in vts.shape)
+    vts.mask = np.asarray(vts.mask, dtype=bool).view(np.ndarray)
+    r = replay.RatslamReplay(pcn=pcn, vts=vts, em=em_ref.ExperienceMap(), batch=False)
+    events = synthetic.ros_stream(n, seed=seed)
+    r.replay_events(events)
+    res = r.results()
+    np.savez_compressed(os.path.join(out, 'ros_replay.npz'), n=np.array(n), seed=np.array(seed),
+                        pc_max=res['pc_max'], em_points=res['em_points'],
+                        template_index=res['template_index'], templates=np.array(res['templates']),
+                        final_state_coo_idx=coo(pcn.posecells)[0], final_state_coo_val=coo(pcn.posecells)[1])
+    print('ros_replay: %d updates, %d frames, %d templates' % (len(res['pc_max']),
+                                                                len(res['template_index']), res['templates']))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default=os.path.dirname(os.path.abspath(__file__)))
+    ap.add_argument('--only', choices=['kernels', 'posecell', 'templates', 'ros_replay'])
     args = ap.parse_args()
     pn, vt = load_reference()
-    gen_kernels(pn, args.out)
-    gen_posecell(pn, args.out)
-    gen_templates(vt, args.out)
+    if args.only in (None, 'kernels'):
+        gen_kernels(pn, args.out)
+    if args.only in (None, 'posecell'):
+        gen_posecell(pn, args.out)
+    if args.only in (None, 'templates'):
+        gen_templates(vt, args.out)
+    if args.only in (None, 'ros_replay'):
+        gen_ros_replay(pn, vt, args.out)
     print('golden vectors written to', args.out)
 
 
