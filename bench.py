@@ -39,6 +39,8 @@ SCAN_KERNELS = {'plane': 'vt_scan_plane_kernel', 'carry': 'vt_scan_carry_kernel'
                 'generic': 'vt_scan_generic_kernel'}
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_COMPARE = 64 * 32  # one stored 64x32 u8 template
+from pyratslam_amd.dist import Dist  # noqa: E402
+
 METRIC = 'pose-cell steps/sec (64×64×36) + template-compares/sec at 1/2/4/8 GPU'
 
 
@@ -61,58 +63,6 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
     return ap.parse_args()
-
-
-class Dist:
-    """Control plane: gloo process group for the barrier, the RCCL unique-id
-    broadcast and the max-over-ranks time.  N = 1 needs no torch at all."""
-
-    def __init__(self, gpus):
-        self.world = int(os.environ.get('WORLD_SIZE', '1'))
-        self.rank = int(os.environ.get('RANK', '0'))
-        self.local = int(os.environ.get('LOCAL_RANK', '0'))
-        if self.world != gpus:
-            raise SystemExit('--gpus %d but WORLD_SIZE=%d: launch N>1 with '
-                             'python -m torch.distributed.run --nproc-per-node N bench.py --gpus N'
-                             % (gpus, self.world))
-        self.dist = None
-        if self.world > 1:
-            import torch.distributed as dist
-            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
-            self.dist = dist
-
-    def barrier(self):
-        if self.dist:
-            self.dist.barrier()
-
-    def bcast_bytes(self, b):
-        if not self.dist:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
-
-    def max(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def min_keys(self, keys):
-        import torch
-        k = torch.from_numpy(keys.astype(np.uint64).view(np.int64).copy())
-        k[k == -1] = np.iinfo(np.int64).max          # UINT64_MAX (no template) -> int64 max
-        self.dist.all_reduce(k, op=self.dist.ReduceOp.MIN)
-        out = k.numpy().copy()
-        out[out == np.iinfo(np.int64).max] = -1
-        return out.view(np.uint64)
-
-    def close(self):
-        if self.dist:
-            self.dist.destroy_process_group()
 
 
 def bench_templates(args, d):

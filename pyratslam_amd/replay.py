@@ -159,29 +159,57 @@ class RatslamReplay:
                 'templates': len(self.vts.templates)}
 
 
+def sharded_templates(d, device, gloo=False, x_range=X_RANGE, y_range=Y_RANGE, x_step=X_STEP,
+                      y_step=Y_STEP, im_size=IM_SIZE, match_threshold=MATCH_THRESHOLD):
+    """The view-template library sharded over the ranks of ``d`` (a dist.Dist):
+    template g on rank g % N, one RCCL allreduce(min) per match (or the gloo
+    host reducer with ``gloo``, for several ranks on one GPU)."""
+    from .view_templates import ShardedViewTemplates
+    if gloo:
+        return ShardedViewTemplates(x_range, y_range, x_step, y_step, im_size[0], im_size[1],
+                                    match_threshold, d.rank, d.world, reducer=d.min_keys, device=device)
+    uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
+    return ShardedViewTemplates(x_range, y_range, x_step, y_step, im_size[0], im_size[1],
+                                match_threshold, d.rank, d.world, reducer='rccl', unique_id=uid,
+                                device=device)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split('\n')[0])
     src = ap.add_mutually_exclusive_group(required=True)
     src.add_argument('--bag', help='ROS 1 bag with navbot/odom and navbot/camera/image')
     src.add_argument('--synthetic', type=int, metavar='N', help='replay N synthetic odometry+frame pairs')
-    ap.add_argument('--device', type=int, default=0)
+    ap.add_argument('--device', type=int, default=None, help='default: LOCAL_RANK')
     ap.add_argument('--precision', default='float32')
     ap.add_argument('--feedback', type=float, default=None,
                     help='inject this energy at each matched template (ros_simulate.py:107-108)')
+    ap.add_argument('--gpus', type=int, default=1,
+                    help='ranks under torch.distributed.run: the template library is sharded '
+                         'over them, the pose cells are replicated')
+    ap.add_argument('--gloo', action='store_true',
+                    help='combine the ranks\' keys on the host (several ranks on one GPU)')
     args = ap.parse_args(argv)
-    r = RatslamReplay(device=args.device, precision=args.precision, feedback_energy=args.feedback)
+    from .dist import Dist
+    d = Dist(args.gpus)
+    dev = d.local if args.device is None else args.device
+    vts = sharded_templates(d, dev, args.gloo) if d.world > 1 else None
+    r = RatslamReplay(device=dev, precision=args.precision, feedback_energy=args.feedback, vts=vts)
+    d.barrier()
     t0 = time.perf_counter()
     if args.bag:
         r.replay_bag(args.bag)
     else:
         from . import synthetic
         r.replay_events(synthetic.ros_stream(args.synthetic))
-    dt = time.perf_counter() - t0
+    dt = d.max(time.perf_counter() - t0)
     res = r.results()
-    print(json.dumps({'updates': len(res['pc_max']), 'frames': len(res['template_index']),
-                      'templates': res['templates'], 'seconds': dt,
-                      'final_pc_max': res['pc_max'][-1].tolist() if len(res['pc_max']) else None,
-                      'final_em_point': res['em_points'][-1].tolist() if len(res['em_points']) else None}))
+    if d.rank == 0:
+        print(json.dumps({'ranks': d.world, 'updates': len(res['pc_max']),
+                          'frames': len(res['template_index']), 'templates': res['templates'],
+                          'seconds': dt, 'pc_max': res['pc_max'].tolist(),
+                          'template_index': res['template_index'].tolist(),
+                          'em_points': res['em_points'].tolist()}))
+    d.close()
     return 0
 
 
