@@ -59,6 +59,9 @@ def parse():
                     help='configs[3] stencil-stress grid, reported beside the headline grid')
     ap.add_argument('--pc-stress-steps', type=int, default=400)
     ap.add_argument('--no-pc-stress', action='store_true')
+    ap.add_argument('--replay-messages', type=int, default=600,
+                    help='configs[4] replay: odometry messages (each followed by a frame)')
+    ap.add_argument('--no-replay', action='store_true')
     ap.add_argument('--cpu-seconds', type=float, default=6.0, help='CPU baseline budget per leg')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
@@ -290,12 +293,36 @@ def cpu_baseline(args):
     return vt, vt_np, pc, pc_np
 
 
+def bench_replay(args, d):
+    """configs[4]: the ROS node's loop (ros_simulate.py:98-162) over a synthetic
+    10 Hz odometry + 256x256 mono8 camera stream (the reference's bag is absent),
+    ROS geometry (21x21x36 pose cells, 32x32 templates); the library is sharded
+    over the ranks (template g on rank g % N), pose cells replicated."""
+    from pyratslam_amd import replay, synthetic
+    events = synthetic.ros_stream(args.replay_messages, seed=0)
+    replay.RatslamReplay(device=d.local).replay_events(events[:40])   # warm-up: kernels, allocations
+    vts = replay.sharded_templates(d, d.local) if d.world > 1 else None
+    r = replay.RatslamReplay(device=d.local, vts=vts)
+    d.barrier()
+    t0 = time.perf_counter()
+    r.replay_events(events)
+    dt = d.max(time.perf_counter() - t0)
+    res = r.results()
+    return {'messages': len(events), 'updates': int(len(res['pc_max'])),
+            'frames': int(len(res['template_index'])), 'templates': int(res['templates']),
+            'seconds': dt, 'messages_per_s': len(events) / dt,
+            'updates_per_s': len(res['pc_max']) / dt, 'frames_per_s': len(res['template_index']) / dt,
+            'note': 'per message: one pose-cell step or one frame match, each a host round trip '
+                    '(the node publishes after every step); synthetic stand-in for dataset_10Hz.bag'}
+
+
 def main():
     args = parse()
     d = Dist(args.gpus)
     tv = bench_templates(args, d)
     pc = bench_posecells(args, d)
     pcs = None if args.no_pc_stress else bench_posecell_stress(args, d)
+    rp = None if args.no_replay else bench_replay(args, d)
     if d.rank != 0:
         d.close()
         return
@@ -323,6 +350,17 @@ def main():
                                     'frac': ach / VALU_PEAK_GINSTS}
         except Exception:
             pass
+    # measured HBM bytes of the pose-cell kernels (same PMC passes), per step form
+    tj_pc = {}
+    if os.path.exists(args.traffic_json):
+        try:
+            tj_pc = json.load(open(args.traffic_json)).get('pose_cell', {})
+        except Exception:
+            tj_pc = {}
+    for leg in (pc, pcs):
+        if leg and leg['step_form'] in tj_pc:
+            leg['roofline']['traffic'] = tj_pc[leg['step_form']]['hbm_bytes_per_step']
+            leg['roofline']['traffic_kernels'] = tj_pc[leg['step_form']]['kernels']
     roof['note'] = ('achieved = 2,048 algorithmic bytes per compare (SURVEY.md 8(d)) / scan time; '
                     'above the HBM peak because each template is read from HBM once per batch and '
                     'reused from registers by all queries (traffic = measured HBM bytes per launch); '
@@ -355,6 +393,7 @@ def main():
         'roofline': roof,
         'pose_cell': pc,
         'pose_cell_stress': pcs,
+        'replay': rp,
         'template_scan': {'kernel': tv['kernel'], 'kernel_ms_per_launch': tv['scan_ms'],
                           'pcie_inclusive_compares_per_s': tv['pcie_inclusive_value'],
                           'known_answer_hits_correct': tv['hits_correct']},

@@ -82,11 +82,25 @@ def main():
     scan = [k for k in kernels if k.startswith('vt_scan') and 'hbm_bytes_per_dispatch' in kernels[k]]
     if scan:
         k = max(scan, key=lambda s: kernels[s]['dispatches'])
+        # pose-cell steps: HBM bytes of one excite + one path dispatch (float32,
+        # batched-run control), per step form -- rows (the 64x64x36 headline grid)
+        # and stream (the 128x128x72 stress grid)
+        pc = {}
+        for form in ('rows', 'stream'):
+            ex = [n for n in kernels if n.startswith(f'pc_excite_{form}<float')
+                  and 'hbm_bytes_per_dispatch' in kernels[n]]
+            pa = [n for n in kernels if n.startswith(f'pc_path_{form}<float') and 'PcCtlRing' in n
+                  and 'hbm_bytes_per_dispatch' in kernels[n]]
+            if ex and pa:
+                ex = max(ex, key=lambda n: kernels[n]['dispatches'])
+                pa = max(pa, key=lambda n: kernels[n]['dispatches'])
+                pc[form] = {'kernels': [ex, pa], 'hbm_bytes_per_step':
+                            kernels[ex]['hbm_bytes_per_dispatch'] + kernels[pa]['hbm_bytes_per_dispatch']}
         with open(os.path.join(a.out, 'pmc_traffic.json'), 'w') as fh:
             json.dump({'kernel': k, 'hbm_bytes_per_launch': kernels[k]['hbm_bytes_per_dispatch'],
                        'valu_insts_per_launch': kernels[k].get('sq', {}).get('SQ_INSTS_VALU'),
                        'templates_per_gpu': a.templates_per_gpu, 'queries': a.queries,
-                       'source': f'{a.round}_pmc_summary.json'}, fh, indent=1)
+                       'pose_cell': pc, 'source': f'{a.round}_pmc_summary.json'}, fh, indent=1)
     lines = [f'# rocprofv3 summary, round {a.round}', '',
              '| kernel | calls | avg us | min us | max us | % time | HBM bytes/dispatch (2*FETCH+WRITE) |',
              '|---|---|---|---|---|---|---|']

@@ -8,7 +8,7 @@ set -euo pipefail
 tag=${1:?tag}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-A="--no-cpu-baseline --steps 5 --warmup 1 --pc-steps 200 --pc-warmup 20 --pc-calls 20"
+A="--no-cpu-baseline --no-replay --steps 5 --warmup 1 --pc-steps 200 --pc-warmup 20 --pc-calls 20 --pc-stress-steps 100"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python bench.py --no-cpu-baseline > gpurun_out/prof_$tag.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python bench.py $A > gpurun_out/pmc_fetch_$tag.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python bench.py $A > gpurun_out/pmc_write_$tag.log 2>&1
