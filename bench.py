@@ -62,6 +62,7 @@ def parse():
     ap.add_argument('--replay-messages', type=int, default=600,
                     help='configs[4] replay: odometry messages (each followed by a frame)')
     ap.add_argument('--no-replay', action='store_true')
+    ap.add_argument('--same-device', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--cpu-seconds', type=float, default=6.0, help='CPU baseline budget per leg')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
@@ -74,18 +75,22 @@ def bench_templates(args, d):
     T, Q, n = args.templates_per_gpu, args.queries, d.world
     reduce_kind = 'none'
     if n == 1:
-        vts = ViewTemplates._from_shape((64, 32), 45000, device=d.local, capacity=T)
+        vts = ViewTemplates._from_shape((64, 32), 45000, device=d.dev, capacity=T)
+    elif args.same_device:  # RCCL refuses two ranks on one GPU: host reducer
+        vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
+                                              device=d.dev, capacity=T)
+        reduce_kind = 'gloo-host-min'
     else:
         uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
         try:
             vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer='rccl',
-                                                  unique_id=uid, device=d.local, capacity=T)
+                                                  unique_id=uid, device=d.dev, capacity=T)
             reduce_kind = 'rccl-allreduce-min-u64'
         except Exception as e:  # pragma: no cover - recorded, not hidden
             print('rank %d: RCCL attach failed (%s); host gloo reduction' % (d.rank, e),
                   file=sys.stderr)
             vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
-                                                  device=d.local, capacity=T)
+                                                  device=d.dev, capacity=T)
             reduce_kind = 'gloo-host-min'
     # every rank adds the whole global library; rank r keeps templates g % n == r
     total = T * n
@@ -165,7 +170,7 @@ def bench_posecell_stress(args, d):
     """configs[3]: the 128x128x72 grid, batched run() steps/s and kernel roofline."""
     from pyratslam_amd import PoseCellNetwork, synthetic
     shape = tuple(int(s) for s in args.pc_stress_shape.split(','))
-    net = PoseCellNetwork(shape, device=d.local)
+    net = PoseCellNetwork(shape, device=d.dev)
     net.inject(1, tuple(s // 2 for s in shape))
     n = args.pc_stress_steps
     od = synthetic.odometry(n + 50, seed=0)
@@ -194,7 +199,7 @@ def bench_posecell_stress(args, d):
 def bench_posecells(args, d):
     from pyratslam_amd import PoseCellNetwork, synthetic
     shape = tuple(int(s) for s in args.pc_shape.split(','))
-    net = PoseCellNetwork(shape, device=d.local)
+    net = PoseCellNetwork(shape, device=d.dev)
     net.inject(1, tuple(s // 2 for s in shape))
     od = synthetic.odometry(args.pc_warmup + args.pc_steps + args.pc_calls + 64, seed=0)
     net.run(od[:args.pc_warmup])
@@ -300,15 +305,23 @@ def bench_replay(args, d):
     over the ranks (template g on rank g % N), pose cells replicated."""
     from pyratslam_amd import replay, synthetic
     events = synthetic.ros_stream(args.replay_messages, seed=0)
-    replay.RatslamReplay(device=d.local).replay_events(events[:40])   # warm-up: kernels, allocations
-    vts = replay.sharded_templates(d, d.local) if d.world > 1 else None
-    r = replay.RatslamReplay(device=d.local, vts=vts)
+    replay.RatslamReplay(device=d.dev).replay_events(events[:40])   # warm-up: kernels, allocations
+    vts, reduce_kind = None, 'none'
+    if d.world > 1 and args.same_device:
+        vts, reduce_kind = replay.sharded_templates(d, d.dev, gloo=True), 'gloo-host-min'
+    elif d.world > 1:
+        try:
+            vts, reduce_kind = replay.sharded_templates(d, d.dev), 'rccl-allreduce-min-u64'
+        except Exception as e:  # pragma: no cover - recorded, not hidden
+            print('rank %d: RCCL attach failed (%s); host gloo reduction' % (d.rank, e), file=sys.stderr)
+            vts, reduce_kind = replay.sharded_templates(d, d.dev, gloo=True), 'gloo-host-min'
+    r = replay.RatslamReplay(device=d.dev, vts=vts)
     d.barrier()
     t0 = time.perf_counter()
     r.replay_events(events)
     dt = d.max(time.perf_counter() - t0)
     res = r.results()
-    return {'messages': len(events), 'updates': int(len(res['pc_max'])),
+    return {'messages': len(events), 'updates': int(len(res['pc_max'])), 'reduce': reduce_kind,
             'frames': int(len(res['template_index'])), 'templates': int(res['templates']),
             'seconds': dt, 'messages_per_s': len(events) / dt,
             'updates_per_s': len(res['pc_max']) / dt, 'frames_per_s': len(res['template_index']) / dt,
@@ -319,6 +332,9 @@ def bench_replay(args, d):
 def main():
     args = parse()
     d = Dist(args.gpus)
+    # the GPU of this rank; --same-device puts every rank on GPU 0 (a test aid for
+    # 1-GPU boxes: RCCL refuses two ranks on one GPU, so the host reducer is used)
+    d.dev = 0 if args.same_device else d.local
     tv = bench_templates(args, d)
     pc = bench_posecells(args, d)
     pcs = None if args.no_pc_stress else bench_posecell_stress(args, d)

@@ -1632,8 +1632,10 @@ int rs_vt_attach_comm(rs_vt* h, int rank, int nranks, const uint8_t id[RS_UNIQUE
     if (nranks > 1) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        ncclResult_t r = ncclCommInitRank(&h->comm, nranks, u, rank);
+        ncclComm_t comm = nullptr;  // kept only on success: destroy never sees a failed init
+        ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);
         RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
+        h->comm = comm;
     }
     h->rank = rank;
     h->nranks = nranks;
