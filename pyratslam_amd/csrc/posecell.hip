@@ -712,31 +712,17 @@ __device__ inline int st_tile(int b, int nb) {
     return (b & 7) * (nb >> 3) + (b >> 3);
 }
 
-// Window loads issued by hand.  The compiler's vmcnt pass cannot follow the
-// 7-slot register ring around the layer loop (it waits for every prefetch at
-// every stage, which collapses the pipeline to one layer), so the window loads
-// are inline asm (saddr form: wave-uniform layer base + 32-bit byte offset) and
-// each stage waits for exactly its own slot.  Nothing else in the loop touches
-// vector memory (outputs are buffered in LDS), and loads return in issue order.
+// Window loads.  Plain loads: hipcc counts them and places the waits.  (An
+// earlier inline-asm form with hand-placed vmcnt waits is unsafe: hipcc treats an
+// asm load's destination as written at the statement and may copy or reuse that
+// register before the data lands.  It was the suspected cause of an illegal-address
+// fault with two processes on one GPU; the plain form measures within 2%.)
 template <typename T>
 __device__ inline T st_load(const T* base, unsigned idx) {
 #ifdef PC_DIAG_NOLOAD  // diagnostic build of tools/pc_probe.hip only: no window traffic
     return (T)(idx & 7) * (T)1e-3;
 #endif
-    T v;
-    const unsigned boff = idx * (unsigned)sizeof(T);
-    if constexpr (sizeof(T) == 4)
-        asm volatile("global_load_dword %0, %1, %2" : "=v"(v) : "v"(boff), "s"(base) : "memory");
-    else
-        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(v) : "v"(boff), "s"(base) : "memory");
-    return v;
-}
-// wait until at most N window loads are in flight; uses of v[] stay after the wait
-template <int N, typename T, int L>
-__device__ inline void st_wait(T (&v)[L]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#pragma unroll
-    for (int u = 0; u < L; ++u) asm volatile("" : "+v"(v[u]));
+    return base[idx];
 }
 
 // Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
@@ -788,7 +774,6 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_excite_stream(con
     // software-pipelined over layers, one barrier per iteration: iteration it
     // stores window it+1, runs the y pass of layer it and the x / theta passes of
     // layer it-1 (its y pass landed before the previous barrier)
-    st_wait<(ST_PF - 1) * LPT>(pre[0]);
 #pragma unroll
     for (int u = 0; u < LPT; ++u) s_in[0][tid + u * NT] = pre[0][u];
     {
@@ -806,8 +791,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_excite_stream(con
             if (it < nL) {
                 const int b = it & 1;
                 // window it+1 (layers past the chunk are valid wrapped addresses: every
-                // load is issued, so the vmcnt count always holds)
-                st_wait<(ST_PF - 1) * LPT>(pre[(s + 1) % FL]);
+                // load is issued, so the counted waits stay in step)
 #pragma unroll
                 for (int u = 0; u < LPT; ++u) s_in[b ^ 1][tid + u * NT] = pre[(s + 1) % FL][u];
                 {
@@ -996,7 +980,6 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     unsigned bl = 0xFFFFFFFFu;
     // software-pipelined: iteration it stores window it+1 while filtering window it;
     // one barrier per iteration
-    st_wait<(ST_PF - 1) * LPT>(pre[0]);
 #pragma unroll
     for (int u = 0; u < LPT; ++u) s_win[0][tid + u * NT] = pre[0][u];
     load(ST_PF, pre[ST_PF % FL]);
@@ -1010,7 +993,6 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
             const int b = it & 1;
             // window it+1 (every load is issued, past the chunk too, so the vmcnt
             // count always holds: see pc_excite_stream)
-            st_wait<(ST_PF - 1) * LPT>(pre[(s + 1) % FL]);
 #pragma unroll
             for (int u = 0; u < LPT; ++u) s_win[b ^ 1][tid + u * NT] = pre[(s + 1) % FL][u];
             load(it + 1 + ST_PF, pre[(s + 1 + ST_PF) % FL]);
