@@ -1079,6 +1079,256 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 }
 
 // One block reduces per-block (value, index) argmax partials into the packed slot.
+// ---------------------------------------------------------------------------
+// Pass form (RS_PC_FORM=passes): the step as four fully parallel passes, one
+// kernel each and no halo recompute:
+//   pc_pass_exy    excitation y and x passes of one layer (posecell_network.py:336)
+//   pc_pass_etheta excitation theta pass, inhibition (:339-340), partial sums (:343)
+//   pc_pass_pxy    the shifted 7x7 path filter of one layer (:273-274) + clamp (:300)
+//   pc_pass_ptheta theta path filter (:310), clamp (:314), normalisation, argmax
+// The xy passes take one 8-row tile of one layer per block, the theta passes
+// four cells per thread, so every kernel holds thousands of waves at any grid
+// size; the price is four launches per step and the E, I and R volumes
+// (L2/MALL-resident at these sizes).  Same arithmetic in the same order as the
+// rows form (y, x, theta; rows then taps).
+// ---------------------------------------------------------------------------
+constexpr int PS_BX = 8;                // rows per xy-pass block, one per wave
+constexpr int PS_NT = 64 * PS_BX;       // 512 threads
+constexpr int PS_CPT = 4;               // cells per thread in the theta passes
+constexpr int PS_CELLS = NT * PS_CPT;   // cells per theta-pass block
+
+// Window rows i0-3 .. i0+10 of one layer, row-shifted by ox and column-shifted
+// by oy (excitation: 0, 0), into LDS with the 3-column wrap halo.
+template <typename T, int YP>
+__device__ __forceinline__ void ps_load_window(const T* __restrict__ plane, T* s_win, int i0, int ox,
+                                               int oy, int X, int Y, int wave, int lane) {
+    constexpr int HX = PS_BX + 2 * HALF, RW = YP + 2 * HALF, JC = YP / 64;
+    T v[2][JC];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int r = min(wave + PS_BX * q, HX - 1);
+        const T* src = plane + (size_t)rs::wrapi(i0 - HALF + r + ox, X) * Y;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) v[q][jc] = src[min(lane + 64 * jc, Y - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int r = wave + PS_BX * q;
+        if (r >= HX) continue;
+        T* dst = s_win + r * RW;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int c = lane + 64 * jc;
+            if (c >= Y) continue;
+            int d = c - oy;
+            if (d < 0) d += Y;
+            dst[HALF + d] = v[q][jc];
+            if (d < HALF) dst[HALF + Y + d] = v[q][jc];
+            if (d >= Y - HALF) dst[d - (Y - HALF)] = v[q][jc];
+        }
+    }
+}
+
+template <typename T, int YP>
+__global__ __launch_bounds__(PS_NT) void pc_pass_exy(const T* __restrict__ P, T* __restrict__ E,
+                                                      T* __restrict__ I,
+                                                      unsigned long long* __restrict__ res_slot,
+                                                      int X, int Y, SepKernel<T> k) {
+    constexpr int HX = PS_BX + 2 * HALF, RW = YP + 2 * HALF, JC = YP / 64;
+    __shared__ T s_in[HX * RW];
+    __shared__ T s_e[HX * YP];
+    __shared__ T s_i[HX * YP];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i0 = blockIdx.x * PS_BX, L = blockIdx.y;
+    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0 && blockIdx.y == 0)
+        res_slot[tid] = 0ull;  // this step's theta path pass max-reduces into them
+    ps_load_window<T, YP>(P + (size_t)L * X * Y, s_in, i0, 0, 0, X, Y, wave, lane);
+    __syncthreads();
+    // y pass (7 taps along the row), two window rows per wave
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int r = wave + PS_BX * q;
+        if (r >= HX) continue;
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            const T* rw = s_in + r * RW + j;
+            T e = 0, g = 0;
+#pragma unroll
+            for (int t = 0; t < FL; ++t) {
+                const T x = rw[t];
+                e += k.ge[t] * x;
+                g += k.gi[t] * x;
+            }
+            s_e[r * YP + j] = e;
+            s_i[r * YP + j] = g;
+        }
+    }
+    __syncthreads();
+    // x pass (7 rows), one output row per wave
+    const int gi = i0 + wave;
+    if (gi >= X) return;
+#pragma unroll
+    for (int jc = 0; jc < JC; ++jc) {
+        const int j = lane + 64 * jc;
+        if (j >= Y) continue;
+        T e = 0, g = 0;
+#pragma unroll
+        for (int t = 0; t < FL; ++t) {
+            e += k.ge[t] * s_e[(wave + t) * YP + j];
+            g += k.gi[t] * s_i[(wave + t) * YP + j];
+        }
+        const size_t o = ((size_t)L * X + gi) * Y + j;
+        E[o] = e;
+        I[o] = g;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void pc_pass_etheta(const T* __restrict__ E, const T* __restrict__ I,
+                                                      T* __restrict__ Q, double* __restrict__ part,
+                                                      unsigned XY, int TH, SepKernel<T> k) {
+    __shared__ double s_red[NT / 64];
+    const unsigned n = XY * (unsigned)TH;
+    double sum = 0.0;
+#pragma unroll
+    for (int u = 0; u < PS_CPT; ++u) {
+        const unsigned c = blockIdx.x * PS_CELLS + u * NT + threadIdx.x;
+        if (c >= n) continue;
+        const int kk = (int)(c / XY);
+        const unsigned xy = c - (unsigned)kk * XY;
+        int l = kk - HALF < 0 ? kk - HALF + TH : kk - HALF;
+        T e = 0, g = 0;
+#pragma unroll
+        for (int t = 0; t < FL; ++t) {
+            const unsigned src = (unsigned)l * XY + xy;
+            e += k.ge[t] * E[src];
+            g += k.gi[t] * I[src];
+            l = l + 1 == TH ? 0 : l + 1;
+        }
+        const T val = (e - g) * k.scale;
+        const T q = (val < k.inhib) ? T(0) : val - k.inhib;
+        Q[c] = q;
+        sum += (double)q;
+    }
+    sum = block_sum(sum, s_red);
+    if (threadIdx.x == 0) part[blockIdx.x] = sum;
+}
+
+template <typename T, int YP, typename CTL>
+__global__ __launch_bounds__(PS_NT) void pc_pass_pxy(const T* __restrict__ Q, T* __restrict__ R,
+                                                      const T* __restrict__ filt, CTL ctl,
+                                                      const double* __restrict__ part, int npart,
+                                                      double* __restrict__ total, int X, int Y) {
+    constexpr int HX = PS_BX + 2 * HALF, RW = YP + 2 * HALF, JC = YP / 64;
+    __shared__ T s_win[HX * RW];
+    __shared__ T s_f[FT];
+    __shared__ double s_red[PS_NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i0 = blockIdx.x * PS_BX, L = blockIdx.y;
+    const int ox = rs::wrapi(ctl_ox(ctl, L), X), oy = rs::wrapi(ctl_oy(ctl, L), Y);
+    if (tid < FT) s_f[tid] = filt[(size_t)ctl_fi(ctl, L) * FT + tid];
+    ps_load_window<T, YP>(Q + (size_t)L * X * Y, s_win, i0, ox, oy, X, Y, wave, lane);
+    __syncthreads();
+    const int gi = i0 + wave;
+    if (gi < X) {
+        T f[FT];
+#pragma unroll
+        for (int t = 0; t < FT; ++t) f[t] = s_f[t];
+#pragma unroll
+        for (int jc = 0; jc < JC; ++jc) {
+            const int j = lane + 64 * jc;
+            if (j >= Y) continue;
+            T acc = 0;
+#pragma unroll
+            for (int x = 0; x < FL; ++x) {
+                T w[FL];
+                const T* rw = s_win + (wave + x) * RW + j;
+#pragma unroll
+                for (int t = 0; t < FL; ++t) w[t] = rw[t];
+#pragma unroll
+                for (int t = 0; t < FL; ++t) acc += w[t] * f[x * FL + t];
+            }
+            R[((size_t)L * X + gi) * Y + j] = acc > T(0) ? acc : T(0);
+        }
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0) {  // the normalisation total, for the theta pass
+        double t = 0.0;
+        for (int i = tid; i < npart; i += PS_NT) t += part[i];
+        t = block_sum_w<PS_NT / 64>(t, s_red);
+        if (tid == 0) *total = t;
+    }
+}
+
+template <typename T, typename CTL>
+__global__ __launch_bounds__(NT) void pc_pass_ptheta(const T* __restrict__ R, T* __restrict__ P, CTL ctl,
+                                                      const double* __restrict__ total,
+                                                      unsigned long long* __restrict__ res_slot,
+                                                      T* __restrict__ bmax, unsigned* __restrict__ bidx,
+                                                      unsigned XY, int TH) {
+    __shared__ T s_bv[NT / 64];
+    __shared__ unsigned s_bl[NT / 64];
+    const unsigned n = XY * (unsigned)TH;
+    const double tot = *total;
+    const T tt = (T)tot;
+    T zf[FL];
+#pragma unroll
+    for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < PS_CPT; ++u) {
+        const unsigned c = blockIdx.x * PS_CELLS + u * NT + threadIdx.x;
+        if (c >= n) continue;
+        const int kk = (int)(c / XY);
+        const unsigned xy = c - (unsigned)kk * XY;
+        int l = kk - HALF < 0 ? kk - HALF + TH : kk - HALF;
+        T acc = 0;
+#pragma unroll
+        for (int z = 0; z < FL; ++z) {
+            acc += R[(unsigned)l * XY + xy] * zf[z];
+            l = l + 1 == TH ? 0 : l + 1;
+        }
+        T val = acc > T(0) ? acc : T(0);
+        if (tot != 0.0) val = val / tt;
+        P[c] = val;
+        const unsigned lin = xy * (unsigned)TH + (unsigned)kk;
+        if (val > bv || (val == bv && lin < bl)) {
+            bv = val;
+            bl = lin;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const T ov = __shfl_xor(bv, off);
+        const unsigned ol = __shfl_xor(bl, off);
+        if (ov > bv || (ov == bv && ol < bl)) {
+            bv = ov;
+            bl = ol;
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_bv[wave] = bv;
+        s_bl[wave] = bl;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < NT / 64; ++w)
+            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                bv = s_bv[w];
+                bl = s_bl[w];
+            }
+        if constexpr (sizeof(T) == 4) {
+            atomicMax(res_slot + (blockIdx.x & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
+        } else {
+            bmax[blockIdx.x] = bv;
+            bidx[blockIdx.x] = bl;
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ bmax,
                                                          const unsigned* __restrict__ bidx, int nb,
@@ -1271,6 +1521,9 @@ struct rs_pc {
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
+    bool passes = false;    // four-pass form (RS_PC_FORM=passes)
+    void* dE = nullptr;     // pass form: excitation y/x passes (E, I)
+    void* dI = nullptr;
 };
 
 namespace {
@@ -1422,6 +1675,35 @@ int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->streamed) {
         RS_TRY((pc_launch_stream<T, CTL>(h, P, Q, slot, bmax, bidx, ctl, prof_base)));
+    } else if (h->passes) {
+        const dim3 gxy((h->X + PS_BX - 1) / PS_BX, h->TH);
+        const dim3 gc((unsigned)((h->n + PS_CELLS - 1) / PS_CELLS));
+        const unsigned XY = (unsigned)h->X * (unsigned)h->Y;
+        T* E = static_cast<T*>(h->dE);
+        T* I = static_cast<T*>(h->dI);
+        T* R = reinterpret_cast<T*>(h->dTmp);
+        if (h->tiling == 64)
+            hipLaunchKernelGGL((pc_pass_exy<T, 64>), gxy, dim3(PS_NT), 0, h->stream, P, E, I, slot,
+                               h->X, h->Y, k);
+        else
+            hipLaunchKernelGGL((pc_pass_exy<T, 128>), gxy, dim3(PS_NT), 0, h->stream, P, E, I, slot,
+                               h->X, h->Y, k);
+        RS_HIP(hipGetLastError());
+        hipLaunchKernelGGL((pc_pass_etheta<T>), gc, dim3(NT), 0, h->stream, E, I, Q, h->dPart, XY,
+                           h->TH, k);
+        RS_HIP(hipGetLastError());
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+        if (!ctl) return RS_OK;
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+        if (h->tiling == 64)
+            hipLaunchKernelGGL((pc_pass_pxy<T, 64, CTL>), gxy, dim3(PS_NT), 0, h->stream, Q, R, filt,
+                               *ctl, h->dPart, h->nPart, h->dScalar, h->X, h->Y);
+        else
+            hipLaunchKernelGGL((pc_pass_pxy<T, 128, CTL>), gxy, dim3(PS_NT), 0, h->stream, Q, R, filt,
+                               *ctl, h->dPart, h->nPart, h->dScalar, h->X, h->Y);
+        RS_HIP(hipGetLastError());
+        hipLaunchKernelGGL((pc_pass_ptheta<T, CTL>), gc, dim3(NT), 0, h->stream, R,
+                           static_cast<T*>(h->dP), *ctl, h->dScalar, slot, bmax, bidx, XY, h->TH);
     } else if (h->tiling == 64 || h->tiling == 128) {
         const dim3 g((h->X + RT_BX - 1) / RT_BX, (h->TH + RT_BK - 1) / RT_BK);
         if (h->tiling == 64)
@@ -1580,9 +1862,8 @@ __global__ void pc_scale_kernel(T* __restrict__ P, size_t n, const double* __res
 // 8 row groups of BX rows; KC (layers per block) is the smallest chunk that keeps
 // the grid within ~2 blocks per CU (fewer, longer blocks re-evaluate fewer halo
 // layers).  RS_PC_FORM=rows|tiles|stream:BX,WR[,KC] overrides (A/B, tests).
-// The streaming kernels count their own window loads with explicit vmcnt waits,
-// which is only sound when the compiler puts no other vector-memory traffic in
-// the layer loop: refuse a variant that spills to scratch.
+// Scratch traffic in the layer loop defeats the streaming kernels' prefetch
+// pipeline: refuse a variant that spills.
 template <typename T>
 int pc_stream_scratch(int bx, int wr, int wc, size_t* bytes) {
     hipFuncAttributes a{};
@@ -1613,6 +1894,12 @@ int pc_choose_form(rs_pc* h) {
         h->streamed = false;
         return RS_OK;
     }
+    if (env && std::strcmp(env, "passes") == 0) {
+        RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=passes needs Y <= 128");
+        h->streamed = false;
+        h->passes = true;
+        return RS_OK;
+    }
     if (env && std::strcmp(env, "tiles") == 0) {
         h->streamed = false;
         h->tiling = 0;
@@ -1624,7 +1911,7 @@ int pc_choose_form(rs_pc* h) {
         RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR,WC[,KC]])", env);
+                 "unknown RS_PC_FORM '%s' (rows | passes | tiles | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
@@ -1724,6 +2011,9 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     if (h->streamed) {
         h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;
         h->nPathBlocks = h->nPart;
+    } else if (h->passes) {
+        h->nPart = (int)((h->n + PS_CELLS - 1) / PS_CELLS);
+        h->nPathBlocks = h->nPart;
     } else if (h->tiling) {
         h->nPart = ((X + RT_BX - 1) / RT_BX) * ((TH + RT_BK - 1) / RT_BK);
         h->nPathBlocks = h->nPart;
@@ -1753,6 +2043,10 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
     PC_ALLOC(hipMalloc(&h->dScalar, sizeof(double)));
+    if (h->passes) {
+        PC_ALLOC(hipMalloc(&h->dE, h->n * h->esz));
+        PC_ALLOC(hipMalloc(&h->dI, h->n * h->esz));
+    }
     PC_ALLOC(hipMalloc(&h->dFilt, h->esz * FT * h->nf));
     if (h->prec == RS_PREC_F32) {
         std::vector<float> f(FT * (size_t)h->nf);
@@ -1782,7 +2076,7 @@ int rs_pc_destroy(rs_pc* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
-                    (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
+                    (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar, h->dE, h->dI})
         if (p) (void)hipFree(p);
     if (h->hRes) (void)hipHostFree(h->hRes);
     if (h->hCtl) (void)hipHostFree(h->hCtl);
@@ -1930,6 +2224,7 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
 const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
     if (h->streamed) return "stream";
+    if (h->passes) return "passes";
     return h->tiling ? "rows" : "tiles";
 }
 

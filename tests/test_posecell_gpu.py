@@ -188,12 +188,12 @@ def test_simulate_driver(pcn):
 
 
 # every step-kernel form (RS_PC_FORM) against the oracle: the row-tiled and 3-D
-# tiled single-pass forms and the layer-streaming form at several tile shapes
+# tiled single-pass forms, the four-pass form and the layer-streaming form at several tile shapes
 # (rows per wave, row groups, layers per block), incl. ragged tiles and grids
 # whose theta extent is not a multiple of the chunk
-FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
+FORMS = {'float32': ['rows', 'passes', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
                      'stream:1,4,2,3', 'stream:2,4,2,6'],
-         'float64': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
+         'float64': ['rows', 'passes', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
