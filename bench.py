@@ -8,6 +8,8 @@ One JSON line on rank 0:
                per rank, sharded round-robin, first-argmin combined by one RCCL
                allreduce(min, uint64) per batch).  Weak scaling: the library
                grows with the number of GPUs.
+  library_sharded  configs[2]: a fixed 100k-template library sharded over the
+               ranks (strong scaling), same query batches and allreduce.
   pose_cell    64x64x36 pose-cell network steps/s (the other half of the
                metric): batched `run()` (per-step control uploaded with the
                odometry) and the per-call `update()` drop-in rate; replicated
@@ -51,6 +53,9 @@ def parse():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--queries', type=int, default=1024)
     ap.add_argument('--templates-per-gpu', type=int, default=1000)
+    ap.add_argument('--library-total', type=int, default=100000,
+                    help='configs[2]: fixed library sharded over the ranks (strong scaling); 0 = off')
+    ap.add_argument('--library-steps', type=int, default=5)
     ap.add_argument('--pc-shape', default='64,64,36')
     ap.add_argument('--pc-steps', type=int, default=2000, help='timed pose-cell steps')
     ap.add_argument('--pc-warmup', type=int, default=200)
@@ -69,10 +74,19 @@ def parse():
     return ap.parse_args()
 
 
-def bench_templates(args, d):
+def bench_templates(args, d, total=None, steps=None, warmup=None):
+    """Frozen-library template matching.  Default (configs[1]): `--templates-per-gpu`
+    templates on every rank (weak scaling).  With `total` (configs[2]): a fixed
+    library of `total` templates sharded over the ranks (strong scaling)."""
     from pyratslam_amd import _lib, synthetic
     from pyratslam_amd.view_templates import ShardedViewTemplates, ViewTemplates
-    T, Q, n = args.templates_per_gpu, args.queries, d.world
+    Q, n = args.queries, d.world
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    if total is None:
+        T, total = args.templates_per_gpu, args.templates_per_gpu * n
+    else:
+        T = (total + n - 1) // n             # rank r holds templates g % n == r
     reduce_kind = 'none'
     if n == 1:
         vts = ViewTemplates._from_shape((64, 32), 45000, device=d.dev, capacity=T)
@@ -93,7 +107,6 @@ def bench_templates(args, d):
                                                   device=d.dev, capacity=T)
             reduce_kind = 'gloo-host-min'
     # every rank adds the whole global library; rank r keeps templates g % n == r
-    total = T * n
     for lo in range(0, total, 8192):
         vts.add(synthetic.library(min(8192, total - lo), seed=1, first=lo))
     qlib = synthetic.library(min(total, 4096), seed=1)
@@ -122,12 +135,12 @@ def bench_templates(args, d):
     match(staged=False)                      # stage the batch in HBM (+ correctness probe)
     hits = src >= 0
     correct = bool(np.all(idx[hits] == src[hits]))
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         match(staged=True)
     kernel_ms = []
     d.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         match(staged=True)
         kernel_ms.append(vts.device_ms())
     t1 = time.perf_counter()
@@ -136,7 +149,8 @@ def bench_templates(args, d):
     # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
     d.barrier()
     p0 = time.perf_counter()
-    for _ in range(max(3, args.steps // 4)):
+    npcie = max(3, steps // 4)
+    for _ in range(npcie):
         match(staged=False)
     p1 = time.perf_counter()
     d.barrier()
@@ -144,12 +158,12 @@ def bench_templates(args, d):
     compares = float(total) * Q
     scan_ms = float(np.mean(kernel_ms))
     res = {
-        'value': compares * args.steps / dt,
-        'ms_per_step': 1e3 * dt / args.steps,
-        'pcie_inclusive_value': compares * max(3, args.steps // 4) / dtp,
+        'value': compares * steps / dt,
+        'ms_per_step': 1e3 * dt / steps,
+        'pcie_inclusive_value': compares * npcie / dtp,
         'scan_ms': scan_ms,
         'kernel': SCAN_KERNELS[vts.scan_form()],
-        'compares_per_launch': float(T) * Q,
+        'compares_per_launch': float(len(range(d.rank, total, n))) * Q,
         'reduce': reduce_kind,
         'hits_correct': correct,
         'templates_total': total,
@@ -336,6 +350,10 @@ def main():
     # 1-GPU boxes: RCCL refuses two ranks on one GPU, so the host reducer is used)
     d.dev = 0 if args.same_device else d.local
     tv = bench_templates(args, d)
+    lib100 = None
+    if args.library_total > 0:
+        lib100 = bench_templates(args, d, total=args.library_total, steps=args.library_steps,
+                                 warmup=1)
     pc = bench_posecells(args, d)
     pcs = None if args.no_pc_stress else bench_posecell_stress(args, d)
     rp = None if args.no_replay else bench_replay(args, d)
@@ -407,6 +425,16 @@ def main():
                            % (d.world, tv['reduce']),
         },
         'roofline': roof,
+        'library_sharded': None if lib100 is None else {
+            'workload': 'configs[2]: %d stored 64x32 u8 templates in total, sharded round-robin '
+                        'over %d GPU(s), %d-query batches resident in HBM' % (
+                            lib100['templates_total'], d.world, args.queries),
+            'scaling': 'strong', 'compares_per_s': lib100['value'],
+            'ms_per_step': lib100['ms_per_step'], 'steps': args.library_steps,
+            'scan_ms_per_launch': lib100['scan_ms'], 'kernel': lib100['kernel'],
+            'compares_per_launch_per_gpu': lib100['compares_per_launch'],
+            'reduce': lib100['reduce'], 'known_answer_hits_correct': lib100['hits_correct'],
+            'pcie_inclusive_compares_per_s': lib100['pcie_inclusive_value']},
         'pose_cell': pc,
         'pose_cell_stress': pcs,
         'replay': rp,
