@@ -1329,6 +1329,20 @@ __global__ __launch_bounds__(NT) void pc_pass_ptheta(const T* __restrict__ R, T*
     }
 }
 
+// Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
+// pinned host buffer (system-scope stores): one queued launch in place of a
+// device-to-host blit copy, which trailed the step by ~10 us (gap + copy kernel).
+__global__ __launch_bounds__(64) void pc_res_export(const unsigned long long* __restrict__ res, int n,
+                                                    unsigned long long* host) {
+    for (int s = blockIdx.x * 64 + threadIdx.x; s < n; s += gridDim.x * 64) {
+        const unsigned long long* r = res + (size_t)s * RES_SLOTS;
+        unsigned long long m = r[0];
+#pragma unroll
+        for (int k = 1; k < RES_SLOTS; ++k) m = r[k] > m ? r[k] : m;
+        __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ bmax,
                                                          const unsigned* __restrict__ bidx, int nb,
@@ -1504,6 +1518,7 @@ struct rs_pc {
     void* dArgV = nullptr;        // per-step per-block argmax partials [resCap][nPathBlocks]
     unsigned* dArgI = nullptr;
     unsigned long long* hRes = nullptr;  // pinned
+    unsigned long long* hResDev = nullptr;  // hRes in the device's address space (pc_res_export)
     unsigned char* dCtl = nullptr;
     unsigned char* hCtl = nullptr;       // pinned
     size_t ctlStride = 0;
@@ -1538,13 +1553,14 @@ int pc_grow_steps(rs_pc* h, int n) {
     if (h->hRes) RS_HIP(hipHostFree(h->hRes));
     if (h->dArgV) RS_HIP(hipFree(h->dArgV));
     if (h->dArgI) RS_HIP(hipFree(h->dArgI));
-    h->dCtl = nullptr; h->hCtl = nullptr; h->dRes = nullptr; h->hRes = nullptr;
+    h->dCtl = nullptr; h->hCtl = nullptr; h->dRes = nullptr; h->hRes = nullptr; h->hResDev = nullptr;
     h->dArgV = nullptr; h->dArgI = nullptr;
     RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
     RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
     RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * RES_SLOTS * cap,
                          hipHostMallocDefault));
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hResDev), h->hRes, 0));
     if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
         RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
         RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
@@ -1744,12 +1760,6 @@ int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     return RS_OK;
 }
 
-unsigned long long slot_max(const unsigned long long* r) {
-    unsigned long long m = r[0];
-    for (int i = 1; i < RES_SLOTS; ++i) m = r[i] > m ? r[i] : m;
-    return m;
-}
-
 void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out) {
     const unsigned lin = 0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull);
     out[2] = (int32_t)(lin % (unsigned)h->TH);
@@ -1796,9 +1806,10 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                            static_cast<const double*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
         RS_HIP(hipGetLastError());
     }
+    hipLaunchKernelGGL(pc_res_export, dim3((n + 63) / 64 < 64 ? (n + 63) / 64 : 64), dim3(64), 0,
+                       h->stream, h->dRes, n, h->hResDev);
+    RS_HIP(hipGetLastError());
     RS_HIP(hipEventRecord(h->ev1, h->stream));
-    RS_HIP(hipMemcpyAsync(h->hRes, h->dRes, sizeof(unsigned long long) * RES_SLOTS * n,
-                          hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     if (h->profiling) {
@@ -1813,7 +1824,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     }
     if (out_xyz)
         for (int s = 0; s < n; ++s)
-            decode_xyz(h, slot_max(h->hRes + (size_t)s * RES_SLOTS), out_xyz + 3 * (size_t)s);
+            decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
     return RS_OK;
 }
 

@@ -806,9 +806,12 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
                           unsigned* __restrict__ next_batch, ScanOut out, int rank, int nranks) {
     static_assert(PL_SPLIT == 2, "two row ranges");
     __shared__ PlaneLds<H> L;
-    // XCD-aware: blocks b and b+8 share an XCD (and its L2); with nqc >= 8 the query
-    // batches are split into 8 groups by XCD, so each L2 holds one group's planes
-    const int tb = (nqc >= 8 ? (int)(blockIdx.x >> 3) : (int)blockIdx.x) % ntb;
+    // The nqc blocks of a template block are adjacent block ids, so they are dispatched
+    // together and split its query batches dynamically even when the grid runs in
+    // several rounds.  XCD-aware: blocks b and b+8 share an XCD (and its L2); with
+    // nqc >= 8 (a multiple of 8) the query batches are split into 8 groups by XCD, so
+    // each L2 holds one group's planes
+    const int tb = (int)(blockIdx.x / (unsigned)nqc);
     const int G = nqc >= 8 ? 8 : 1, g = nqc >= 8 ? (int)(blockIdx.x & 7) : 0;
     unsigned* ctr = next_batch + (size_t)tb * 8 + g;
     VT_STAMP(0);
@@ -829,6 +832,17 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     // user in this launch: it rewinds the counter for the next launch (no memset).
     if (threadIdx.x == 0 && L.batch == ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G + nqc / G - 1) *ctr = 0u;
     VT_STAMP(1);
+}
+
+// The batch's first-argmin keys -> the pinned host buffer (system-scope stores),
+// and the device keys reset to UINT64_MAX for the next scan: one queued launch in
+// place of a device-to-host blit copy and a memset before the next scan.
+__global__ __launch_bounds__(256) void vt_keys_export(unsigned long long* __restrict__ keys, int n,
+                                                      unsigned long long* host) {
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        __hip_atomic_store(host + i, keys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        keys[i] = ~0ull;
+    }
 }
 
 }  // namespace
@@ -854,6 +868,9 @@ struct rs_vt {
     uint32_t* dQsum = nullptr;
     unsigned long long* dBest = nullptr;
     unsigned long long* hBest = nullptr;  // pinned
+    unsigned long long* hBestDev = nullptr;  // hBest in the device's address space
+    int bestClean = 0;     // leading dBest entries known to hold UINT64_MAX
+    int bestPending = 0;   // bestClean once the keys of the running scan are exported
     // index lists for stores
     int idxCap = 0;
     int32_t* dSrc = nullptr;
@@ -978,6 +995,8 @@ int vt_grow_queries(rs_vt* h, int nq) {
     RS_HIP(hipMalloc(&h->dQsum, sizeof(uint32_t) * cap));
     RS_HIP(hipMalloc(&h->dBest, sizeof(unsigned long long) * cap));
     RS_HIP(hipHostMalloc(&h->hBest, sizeof(unsigned long long) * cap, hipHostMallocDefault));
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hBestDev), h->hBest, 0));
+    h->bestClean = h->bestPending = 0;
     h->qCap = cap;
     return RS_OK;
 }
@@ -1099,16 +1118,34 @@ int vt_store(rs_vt* h, bool cand, const uint8_t* d_raw, int n) {
     return RS_OK;
 }
 
+// Blocks per template block (nqc) for the plane scan.  A block's fixed cost
+// (its template planes, 128 KiB, into VGPRs) is small next to its query batches,
+// and the nqc blocks of a template block balance their batches dynamically, so
+// finer splits fill the last round of resident blocks better; measured on
+// MI355X (tools/scan_split.py, 1,024 queries): nqc = 32 is within 2% of the best
+// split from 12.5k to 100k templates (100k: 18.6 ms at nqc = 1, the previous
+// choice there, vs 15.0 ms), and small libraries gain from up to 4 rounds of
+// blocks (1k: 128 -> 0.183 ms vs 0.199 ms at 32).  nqc >= 8 is a multiple of 8
+// (the XCD query groups).  RS_VT_NQC overrides (A/B).
+int plane_split(int ntb, int nbatch, int slots) {
+    int nqc;
+    if (const char* e = std::getenv("RS_VT_NQC")) {
+        nqc = std::max(1, std::atoi(e));
+    } else {
+        const int fill = (slots + ntb - 1) / ntb;  // blocks per template block for one round
+        nqc = std::max(32, std::min(4 * fill, std::max(128, fill)));
+    }
+    nqc = std::min(nqc, std::max(1, nbatch));
+    if (nqc >= 8) nqc &= ~7;
+    return nqc;
+}
+
 // Launch a scan of queries [0, nq) (forms in dQf) against `count` slots of lib.
 template <bool MATRIX>
 int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
                     int nranks) {
     const int ntb = (int)((count + 63) / 64);
-    // One resident wave of blocks: nqc near-equal query chunks per template block so
-    // that ntb * nqc fills the block slots once (a multiple of 8 keeps the XCD-aware
-    // mapping exact).  Libraries beyond the slot count run ntb blocks of all queries.
-    int nqc = std::max(1, std::min((nq + PL_NB - 1) / PL_NB, h->planeSlots / ntb));
-    if (nqc >= 8) nqc &= ~7;
+    const int nqc = plane_split(ntb, (nq + PL_NB - 1) / PL_NB, h->planeSlots);
     if (8 * ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
         const int cap = std::max(8 * ntb, 2 * h->ctrCap);
         if (h->dCtr) RS_HIP(hipFree(h->dCtr));
@@ -1233,7 +1270,12 @@ int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = f
         RS_CHECK(nq == h->stagedQ, RS_ERR_STATE, "no staged batch of %d queries (have %d)", nq,
                  h->stagedQ);
     }
-    RS_HIP(hipMemsetAsync(h->dBest, 0xFF, sizeof(unsigned long long) * nq, h->stream));
+    if (h->bestClean < nq) {  // vt_keys_export resets the keys it hands over
+        RS_HIP(hipMemsetAsync(h->dBest, 0xFF, sizeof(unsigned long long) * nq, h->stream));
+        h->bestClean = nq;
+    }
+    h->bestPending = h->bestClean;  // [0, nq) is dirty until exported; the rest stays clean
+    h->bestClean = 0;
     const int64_t lc = local_count_of(h, h->count);
     ScanOut out{h->dBest, nullptr, 0};
     RS_HIP(hipEventRecord(h->ev0, h->stream));
@@ -1324,9 +1366,11 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
         RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
                  ncclGetErrorString(r));
     }
-    RS_HIP(hipMemcpyAsync(h->hBest, h->dBest, sizeof(unsigned long long) * nq,
-                          hipMemcpyDeviceToHost, h->stream));
+    hipLaunchKernelGGL(vt_keys_export, dim3((nq + 255) / 256 < 64 ? (nq + 255) / 256 : 64), dim3(256), 0,
+                       h->stream, h->dBest, nq, h->hBestDev);
+    RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
+    h->bestClean = h->bestPending;
     RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     return RS_OK;
 }
