@@ -117,35 +117,42 @@ def bench_templates(args, d, total=None, steps=None, warmup=None):
     score = np.empty(Q, dtype=np.uint64)
     new = np.empty(Q, dtype=np.uint8)
 
+    # result pointers converted once (the arrays are reused every batch)
+    p_score, p_idx, p_new = (_lib.ptr(score, ctypes.c_uint64), _lib.ptr(idx, ctypes.c_int64),
+                             _lib.ptr(new, ctypes.c_uint8))
+    p_queries = _lib.ptr(queries, ctypes.c_uint8)
+
     def match(staged):
-        qp = None if staged else _lib.ptr(queries, ctypes.c_uint8)
+        qp = None if staged else p_queries
         if vts.nranks > 1 and vts.reducer != 'rccl':
             local = np.empty(Q, dtype=np.uint64)
             _lib.check(lib.rs_vt_scan_local(vts._h, Q, qp, _lib.ptr(local, ctypes.c_uint64)))
             glob = np.ascontiguousarray(vts.reducer(local))
             _lib.check(lib.rs_vt_resolve(vts._h, Q, _lib.ptr(glob, ctypes.c_uint64), 0,
-                                         _lib.ptr(score, ctypes.c_uint64),
-                                         _lib.ptr(idx, ctypes.c_int64), _lib.ptr(new, ctypes.c_uint8)))
+                                         p_score, p_idx, p_new))
         else:
-            _lib.check(lib.rs_vt_match_batch(vts._h, Q, qp, _lib.RS_VT_FROZEN,
-                                             _lib.ptr(score, ctypes.c_uint64),
-                                             _lib.ptr(idx, ctypes.c_int64),
-                                             _lib.ptr(new, ctypes.c_uint8)))
+            _lib.check(lib.rs_vt_match_batch(vts._h, Q, qp, _lib.RS_VT_FROZEN, p_score, p_idx, p_new))
 
     match(staged=False)                      # stage the batch in HBM (+ correctness probe)
     hits = src >= 0
     correct = bool(np.all(idx[hits] == src[hits]))
     for _ in range(warmup):
         match(staged=True)
-    kernel_ms = []
+    # the timed batches run without the scan's timing events (two stream markers per
+    # batch); the scan kernel's duration for the roofline comes from a separate timed pass
+    vts.set_timing(False)
     d.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         match(staged=True)
-        kernel_ms.append(vts.device_ms())
     t1 = time.perf_counter()
     d.barrier()
     dt = d.max(t1 - t0)
+    vts.set_timing(True)
+    kernel_ms = []
+    for _ in range(steps):
+        match(staged=True)
+        kernel_ms.append(vts.device_ms())
     # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
     d.barrier()
     p0 = time.perf_counter()

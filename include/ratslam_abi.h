@@ -183,8 +183,12 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
 int rs_vt_scan_local(rs_vt* h, int nq, const uint8_t* queries, uint64_t* local_keys);
 int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint64_t* best_score,
                   int64_t* best_index, uint8_t* is_new);
-/* device time (ms) of the scan kernel in the last match call (HIP events) */
+/* device time (ms) of the scan kernel in the last match call (HIP events);
+ * -1 when that scan ran untimed */
 int rs_vt_last_ms(rs_vt* h, double* ms);
+/* HIP events around every scan (default on); off drops two stream markers per
+ * match call (a ~5 us gap between the scan and the result export) */
+int rs_vt_set_timing(rs_vt* h, int enable);
 /* which scan kernel family the handle uses for its shape: "plane" (bit-plane
  * borrow count, W == 32, H in {32, 64}, max_offset 8), "carry", "sad", "rb2",
  * "rb3" (byte-SWAR forms, RS_VT_SCAN) or "generic"; NULL for a null handle */

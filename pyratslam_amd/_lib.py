@@ -88,6 +88,7 @@ SIGNATURES = {
     'rs_vt_scan_local': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, _u64p]),
     'rs_vt_resolve': (ctypes.c_int, [_vp, ctypes.c_int, _u64p, ctypes.c_int, _u64p, _i64p, _u8p]),
     'rs_vt_last_ms': (ctypes.c_int, [_vp, _f64p]),
+    'rs_vt_set_timing': (ctypes.c_int, [_vp, ctypes.c_int]),
     'rs_vt_scan_form': (ctypes.c_char_p, [_vp]),
     'rs_comm_unique_id': (ctypes.c_int, [_u8p]),
     'rs_vt_attach_comm': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _u8p]),

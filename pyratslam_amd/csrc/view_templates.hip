@@ -884,6 +884,8 @@ struct rs_vt {
     uint32_t* dMat = nullptr;
     uint32_t* hMat = nullptr;  // pinned
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timing = true;  // HIP events around every scan (rs_vt_set_timing)
+    bool timedScan = false;  // the last scan recorded ev0/ev1
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
     bool carry = true;  // carry-count scan or v_sad_u8 scan (RS_VT_SCAN=sad)
@@ -1278,9 +1280,10 @@ int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = f
     h->bestClean = 0;
     const int64_t lc = local_count_of(h, h->count);
     ScanOut out{h->dBest, nullptr, 0};
-    RS_HIP(hipEventRecord(h->ev0, h->stream));
+    if (h->timing) RS_HIP(hipEventRecord(h->ev0, h->stream));
     RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
-    RS_HIP(hipEventRecord(h->ev1, h->stream));
+    if (h->timing) RS_HIP(hipEventRecord(h->ev1, h->stream));
+    h->timedScan = h->timing;
     h->stagedQ = nq;
     return RS_OK;
 }
@@ -1371,7 +1374,7 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
     RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
     h->bestClean = h->bestPending;
-    RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     return RS_OK;
 }
 
@@ -1651,7 +1654,14 @@ const char* rs_vt_scan_form(const rs_vt* h) {
 
 int rs_vt_last_ms(rs_vt* h, double* ms) {
     RS_CHECK(h && ms, RS_ERR_ARG, "null argument");
-    *ms = h->lastMs;
+    *ms = h->timedScan ? h->lastMs : -1.0;
+    return RS_OK;
+}
+
+int rs_vt_set_timing(rs_vt* h, int enable) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    h->timing = enable != 0;
     return RS_OK;
 }
 

@@ -267,9 +267,14 @@ class ViewTemplates:
         return idx, score, new.astype(bool)
 
     def device_ms(self):
+        """Scan kernel time (HIP events) of the last match, ms; -1 if it ran untimed."""
         ms = ctypes.c_double()
         _lib.check(self._lib.rs_vt_last_ms(self._h, ctypes.byref(ms)))
         return ms.value
+
+    def set_timing(self, enable=True):
+        """HIP events around every scan (default on; rs_vt_set_timing)."""
+        _lib.check(self._lib.rs_vt_set_timing(self._h, int(bool(enable))))
 
     def scan_form(self):
         """Scan kernel family used for this shape ('plane', 'carry', 'sad', ...)."""

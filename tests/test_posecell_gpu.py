@@ -43,7 +43,9 @@ def test_golden_trajectory(pcn, name, precision, tol):
 
 
 def test_run_equals_repeated_update(pcn):
-    od = odometry(64, 11)
+    # 4,200 steps in one run(): more results than one pass of the export kernel's
+    # grid (64 blocks x 64 steps), so its grid-stride loop is exercised
+    od = odometry(4200, 11)
     a = pcn((32, 32, 18))
     b = pcn((32, 32, 18))
     a.inject(1, (16, 16, 9))

@@ -1,5 +1,7 @@
 """View-template matcher on the GPU: bit-exact scores and template indices vs the
 reference's golden vectors and the oracle (integer work -> exact equality)."""
+import functools
+
 import numpy as np
 import pytest
 
@@ -100,6 +102,30 @@ def test_scan_variants_vs_oracle(vtmod, monkeypatch, scan, h):
     idx, score, _ = lib.match_templates(queries, mode=0)
     assert np.array_equal(score, ref.min(axis=1))
     assert np.array_equal(idx, ref.argmin(axis=1))
+
+
+@functools.lru_cache(maxsize=1)
+def _split_case():
+    lib_np = V.synthetic_library(700, 64, 32, seed=11)
+    queries, _ = V.synthetic_queries(lib_np, 240, seed=12)
+    return lib_np, queries, np.stack([V.vt_scores_library(lib_np, q) for q in queries])
+
+
+@pytest.mark.parametrize('nqc', ['1', '3', '8', '24', '64', '512'])
+def test_plane_scan_work_splits(vtmod, monkeypatch, nqc):
+    """The plane scan gives the oracle's first argmin whatever the number of
+    blocks per template block (RS_VT_NQC): one block of all queries, split
+    without XCD query groups (3), with them (8, 24, 64), and more blocks than
+    query batches (512, capped at the batch count); the library spans several rounds of resident blocks at
+    the large splits, and a second launch reuses the batch counters."""
+    monkeypatch.setenv('RS_VT_NQC', nqc)
+    lib_np, queries, ref = _split_case()
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    lib.add(lib_np)
+    for _ in range(2):
+        idx, score, _ = lib.match_templates(queries, mode=0)
+        assert np.array_equal(score, ref.min(axis=1))
+        assert np.array_equal(idx, ref.argmin(axis=1))
 
 
 def test_all_pair_scores_vs_oracle(vtmod):
@@ -283,3 +309,18 @@ def test_match_frames_errors(vtmod):
     lone = vtmod.ViewTemplates._from_shape((32, 32), 45000)
     with pytest.raises(ValueError):
         lone.match_frames(np.zeros((1, 256, 256), dtype=np.uint8), None)
+
+
+def test_untimed_scans(vtmod):
+    """rs_vt_set_timing(0) drops the scan's HIP events: same results, no time."""
+    lib_np, queries, ref = _split_case()
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    lib.add(lib_np)
+    lib.set_timing(False)
+    idx, score, _ = lib.match_templates(queries, mode=0)
+    assert np.array_equal(idx, ref.argmin(axis=1)) and np.array_equal(score, ref.min(axis=1))
+    assert lib.device_ms() == -1.0
+    lib.set_timing(True)
+    idx, _, _ = lib.match_templates(queries[:50], mode=0)
+    assert np.array_equal(idx, ref[:50].argmin(axis=1))
+    assert lib.device_ms() > 0.0
