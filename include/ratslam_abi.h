@@ -15,6 +15,9 @@
  *   rs_pc_update    PoseCellNetwork.update        posecell_network.py:326-353
  *                   (conv_im x3 + host inhibition/normalisation/clamps/argmax,
  *                    convolution.py:404-511, posecell_network.py:336-351)
+ *   rs_pc_update_odom / rs_pc_run_odom
+ *                   update(v) / run() taking the odometry itself: path_integration's
+ *                   control (posecell_network.py:252-308) computed in the library
  *   rs_pc_excite    update() steps 1-4 alone      posecell_network.py:336-345
  *   rs_pc_run       a loop of update() calls      simulate.py:31-34, ros_simulate.py:134-137
  *   rs_pc_inject    PoseCellNetwork.inject        posecell_network.py:322-324
@@ -51,6 +54,8 @@ extern "C" {
 #define RS_ERR_RCCL     5   /* RuntimeError (RCCL failure)                           */
 #define RS_ERR_STATE    6   /* RuntimeError (handle misuse)                          */
 #define RS_ERR_NOMEM    7   /* MemoryError                                           */
+#define RS_ERR_CTL_RANGE 8  /* (internal) odometry outside the uploaded control tables;
+                               nothing ran, the caller computes the control itself     */
 
 #define RS_PREC_F32 0
 #define RS_PREC_F64 1
@@ -105,6 +110,32 @@ int rs_pc_update(rs_pc* h, const int32_t* ox, const int32_t* oy, const int32_t* 
 /* n consecutive updates with one host round trip; out_xyz[n*3] (may be NULL) */
 int rs_pc_run(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
               const double* zf, int32_t* out_xyz);
+/* Odometry -> control inside the library (posecell_network.py:252-308), so update()
+ * costs one FFI call and no NumPy.  The wrapper uploads, once, the tables the NumPy
+ * path evaluates with NumPy's own functions -- per-layer cos/sin of the heading
+ * (:257-261), the LUT key -> filter row map (:249), and the 1-D theta filters for
+ * origins zorig_min .. zorig_min+nz-1 (:304-308) -- and the library then applies
+ * only correctly rounded IEEE operations (division, one product, rint, trunc,
+ * floor, no contraction), so the control is bit-identical to filters.step_control.
+ * rs_pc_update_odom: RS_ERR_LUT_KEY after running steps 1-4 (the reference's state
+ * when :249 raises); RS_ERR_CTL_RANGE, with nothing run, when the theta origin is
+ * outside the uploaded filters (the caller then computes the control itself).
+ * rs_pc_run_odom: odom[n*2] = (vtrans, vrot) per step; on a LUT miss at step s it
+ * runs steps < s, then steps 1-4 of s, sets *first_bad = s and returns
+ * RS_ERR_LUT_KEY (else *first_bad = -1). */
+int rs_pc_set_odometry_tables(rs_pc* h, double vtrans_scale, double vrot_scale,
+                              const double* cos_a, const double* sin_a, int key_min,
+                              int nkeys, const int32_t* key_rows, int zorig_min, int nz,
+                              const double* zf_table);
+int rs_pc_update_odom(rs_pc* h, double vtrans, double vrot, int32_t out_xyz[3]);
+/* the same control on the host alone (no handle, no device): n steps of odom[n*2]
+ * -> ox/oy/fidx[n*TH], zf[n*7] and a status per step (RS_OK, RS_ERR_LUT_KEY,
+ * RS_ERR_CTL_RANGE; outputs of a failed step are partial) */
+int rs_pc_odom_control(int TH, double vtrans_scale, double vrot_scale, const double* cos_a,
+                       const double* sin_a, int key_min, int nkeys, const int32_t* key_rows,
+                       int zorig_min, int nz, const double* zf_table, int n, const double* odom,
+                       int32_t* ox, int32_t* oy, int32_t* fidx, double* zf, int32_t* status);
+int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* first_bad);
 /* steps 1-4 of update() alone (excitation, global inhibition, normalisation):
  * the state the reference leaves behind when path_integration raises KeyError */
 int rs_pc_excite(rs_pc* h);

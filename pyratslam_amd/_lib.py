@@ -21,6 +21,7 @@ RS_ERR_HIP = 4
 RS_ERR_RCCL = 5
 RS_ERR_STATE = 6
 RS_ERR_NOMEM = 7
+RS_ERR_CTL_RANGE = 8
 RS_PREC_F32 = 0
 RS_PREC_F64 = 1
 RS_VT_FROZEN = 0
@@ -64,6 +65,15 @@ SIGNATURES = {
     'rs_pc_shape': (ctypes.c_int, [_vp, _c_int_p, _c_int_p, _c_int_p]),
     'rs_pc_update': (ctypes.c_int, [_vp, _i32p, _i32p, _i32p, _f64p, _i32p]),
     'rs_pc_run': (ctypes.c_int, [_vp, ctypes.c_int, _i32p, _i32p, _i32p, _f64p, _i32p]),
+    'rs_pc_set_odometry_tables': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, _f64p, _f64p,
+                                                 ctypes.c_int, ctypes.c_int, _i32p, ctypes.c_int,
+                                                 ctypes.c_int, _f64p]),
+    'rs_pc_update_odom': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, _i32p]),
+    'rs_pc_odom_control': (ctypes.c_int, [ctypes.c_int, ctypes.c_double, ctypes.c_double, _f64p,
+                                          _f64p, ctypes.c_int, ctypes.c_int, _i32p, ctypes.c_int,
+                                          ctypes.c_int, _f64p, ctypes.c_int, _f64p, _i32p, _i32p,
+                                          _i32p, _f64p, _i32p]),
+    'rs_pc_run_odom': (ctypes.c_int, [_vp, ctypes.c_int, _f64p, _i32p, _c_int_p]),
     'rs_pc_excite': (ctypes.c_int, [_vp]),
     'rs_pc_inject': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     'rs_pc_get_max': (ctypes.c_int, [_vp, _i32p]),

@@ -1499,6 +1499,21 @@ __global__ __launch_bounds__(NT) void pc_total_kernel(const T* __restrict__ P, s
 // ===========================================================================
 // Host side
 // ===========================================================================
+// Tables of path_integration's control (rs_pc_set_odometry_tables): NumPy-evaluated
+// cos/sin per layer, the LUT key -> filter row map and the theta filters per origin.
+struct OdoTables {
+    int TH = 0;
+    double vtScale = 0.0, vrScale = 0.0;
+    const double* cosA = nullptr;
+    const double* sinA = nullptr;
+    int keyMin = 0, nKeys = 0;
+    const int32_t* keyRows = nullptr;
+    int zMin = 0, nZ = 0;
+    const double* zfTab = nullptr;
+    std::vector<double> own;        // owned copies when held by a handle
+    std::vector<int32_t> ownRows;
+};
+
 struct rs_pc {
     int X = 0, Y = 0, TH = 0, prec = RS_PREC_F32, device = 0;
     size_t n = 0, esz = 4;
@@ -1539,6 +1554,11 @@ struct rs_pc {
     bool passes = false;    // four-pass form (RS_PC_FORM=passes)
     void* dE = nullptr;     // pass form: excitation y/x passes (E, I)
     void* dI = nullptr;
+    // odometry -> control tables (rs_pc_set_odometry_tables) and per-call scratch
+    bool odoReady = false;
+    OdoTables odo{};
+    std::vector<int32_t> cOx, cOy, cRows;
+    std::vector<double> cZf;
 };
 
 namespace {
@@ -1825,6 +1845,41 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (out_xyz)
         for (int s = 0; s < n; ++s)
             decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
+    return RS_OK;
+}
+
+// path_integration's control for one step (posecell_network.py:252-308) in the
+// operation order of filters.step_control: vt = vtrans/0.2, vr = vrot/(2pi/TH),
+// e = vt*cos|sin (:257-261), o = around(e) (:262-265, half-even = rint), key =
+// int((e_x - o_x)*10) (:246-249), theta origin floor(vr + .5) (:304).  Each is one
+// correctly rounded IEEE operation on the same operands as NumPy's, and
+// contraction is off, so the result is bit-identical.  Returns RS_ERR_LUT_KEY on
+// a key outside the LUT (the reference's KeyError, :249; checked before the theta
+// filter, as the reference builds the xy filters first) and RS_ERR_CTL_RANGE when
+// the theta origin or a shift lies outside what the tables cover.
+constexpr double PC_LUT_PRECISION = 10.0;  // filter_dict_2d_precision, posecell_network.py:48
+
+int pc_odom_control(const OdoTables* h, double vtrans, double vrot, int32_t* ox, int32_t* oy,
+                    int32_t* rows, double* zf) {
+#pragma clang fp contract(off)
+    const double vt = vtrans / h->vtScale;
+    const double vr = vrot / h->vrScale;
+    for (int k = 0; k < h->TH; ++k) {
+        const double ex = vt * h->cosA[k];
+        const double ey = vt * h->sinA[k];
+        const double rx = std::nearbyint(ex);
+        const double ry = std::nearbyint(ey);
+        const double key = std::trunc((ex - rx) * PC_LUT_PRECISION);
+        if (!(key >= h->keyMin && key < h->keyMin + h->nKeys)) return RS_ERR_LUT_KEY;  // NaN too
+        if (!(std::fabs(rx) < 1073741824.0 && std::fabs(ry) < 1073741824.0)) return RS_ERR_CTL_RANGE;
+        ox[k] = (int32_t)rx;
+        oy[k] = (int32_t)ry;
+        rows[k] = h->keyRows[(int)key - h->keyMin];
+    }
+    const double zo = std::floor(vr + 0.5);
+    if (!(zo >= h->zMin && zo < h->zMin + h->nZ)) return RS_ERR_CTL_RANGE;
+    const double* f = h->zfTab + (size_t)((int)zo - h->zMin) * FL;
+    for (int t = 0; t < FL; ++t) zf[t] = f[t];
     return RS_OK;
 }
 
@@ -2135,6 +2190,117 @@ int rs_pc_excite(rs_pc* h) {
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
+int rs_pc_set_odometry_tables(rs_pc* h, double vtrans_scale, double vrot_scale,
+                              const double* cos_a, const double* sin_a, int key_min,
+                              int nkeys, const int32_t* key_rows, int zorig_min, int nz,
+                              const double* zf_table) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(cos_a && sin_a && key_rows && zf_table, RS_ERR_ARG, "null table");
+    RS_CHECK(nkeys > 0 && nz > 0, RS_ERR_ARG, "empty key or theta-filter table");
+    RS_CHECK(vtrans_scale != 0.0 && vrot_scale != 0.0, RS_ERR_ARG, "zero odometry scale");
+    for (int i = 0; i < nkeys; ++i)
+        RS_CHECK(key_rows[i] >= 0 && key_rows[i] < h->nf, RS_ERR_ARG,
+                 "key row %d outside the %d-filter table", key_rows[i], h->nf);
+    OdoTables& o = h->odo;
+    o.TH = h->TH;
+    o.vtScale = vtrans_scale;
+    o.vrScale = vrot_scale;
+    o.own.assign(cos_a, cos_a + h->TH);
+    o.own.insert(o.own.end(), sin_a, sin_a + h->TH);
+    o.own.insert(o.own.end(), zf_table, zf_table + (size_t)nz * FL);
+    o.ownRows.assign(key_rows, key_rows + nkeys);
+    o.cosA = o.own.data();
+    o.sinA = o.own.data() + h->TH;
+    o.zfTab = o.own.data() + 2 * (size_t)h->TH;
+    o.keyMin = key_min;
+    o.nKeys = nkeys;
+    o.keyRows = o.ownRows.data();
+    o.zMin = zorig_min;
+    o.nZ = nz;
+    h->odoReady = true;
+    return RS_OK;
+}
+
+int rs_pc_odom_control(int TH, double vtrans_scale, double vrot_scale, const double* cos_a,
+                       const double* sin_a, int key_min, int nkeys, const int32_t* key_rows,
+                       int zorig_min, int nz, const double* zf_table, int n, const double* odom,
+                       int32_t* ox, int32_t* oy, int32_t* fidx, double* zf, int32_t* status) {
+    rs::clear_error();
+    RS_CHECK(TH > 0 && n >= 0 && nkeys > 0 && nz > 0, RS_ERR_ARG, "bad table or batch size");
+    RS_CHECK(cos_a && sin_a && key_rows && zf_table && (n == 0 || (odom && ox && oy && fidx && zf &&
+             status)), RS_ERR_ARG, "null argument");
+    OdoTables o;
+    o.TH = TH;
+    o.vtScale = vtrans_scale;
+    o.vrScale = vrot_scale;
+    o.cosA = cos_a;
+    o.sinA = sin_a;
+    o.keyMin = key_min;
+    o.nKeys = nkeys;
+    o.keyRows = key_rows;
+    o.zMin = zorig_min;
+    o.nZ = nz;
+    o.zfTab = zf_table;
+    for (int s = 0; s < n; ++s)
+        status[s] = pc_odom_control(&o, odom[2 * s], odom[2 * s + 1], ox + (size_t)TH * s,
+                                    oy + (size_t)TH * s, fidx + (size_t)TH * s, zf + (size_t)FL * s);
+    return RS_OK;
+}
+
+int rs_pc_update_odom(rs_pc* h, double vtrans, double vrot, int32_t out_xyz[3]) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(h->odoReady, RS_ERR_STATE, "rs_pc_set_odometry_tables has not been called");
+    h->cOx.resize(h->TH);
+    h->cOy.resize(h->TH);
+    h->cRows.resize(h->TH);
+    h->cZf.resize(FL);
+    const int st = pc_odom_control(&h->odo, vtrans, vrot, h->cOx.data(), h->cOy.data(),
+                                   h->cRows.data(), h->cZf.data());
+    if (st == RS_ERR_LUT_KEY) {
+        // the reference raises inside path_integration, after steps 1-4 ran
+        RS_TRY(rs_pc_excite(h));
+        RS_CHECK(false, RS_ERR_LUT_KEY, "path-integration LUT key outside the table "
+                 "(posecell_network.py:249)");
+    }
+    RS_CHECK(st == RS_OK, st, "odometry (%g, %g) outside the control tables", vtrans, vrot);
+    return pc_run_impl(h, 1, h->cOx.data(), h->cOy.data(), h->cRows.data(), h->cZf.data(), out_xyz);
+}
+
+int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* first_bad) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(h->odoReady, RS_ERR_STATE, "rs_pc_set_odometry_tables has not been called");
+    RS_CHECK(n >= 0 && (odom || n == 0), RS_ERR_ARG, "bad odometry batch");
+    if (first_bad) *first_bad = -1;
+    const size_t th = h->TH;
+    h->cOx.resize(th * (n > 0 ? n : 1));
+    h->cOy.resize(th * (n > 0 ? n : 1));
+    h->cRows.resize(th * (n > 0 ? n : 1));
+    h->cZf.resize((size_t)FL * (n > 0 ? n : 1));
+    int todo = n;
+    for (int s = 0; s < n; ++s) {
+        const int st = pc_odom_control(&h->odo, odom[2 * s], odom[2 * s + 1], h->cOx.data() + th * s,
+                                       h->cOy.data() + th * s, h->cRows.data() + th * s,
+                                       h->cZf.data() + (size_t)FL * s);
+        if (st == RS_ERR_LUT_KEY) {
+            todo = s;
+            break;
+        }
+        RS_CHECK(st == RS_OK, st, "odometry of step %d outside the control tables", s);
+    }
+    RS_TRY(pc_run_impl(h, todo, h->cOx.data(), h->cOy.data(), h->cRows.data(), h->cZf.data(),
+                       out_xyz));
+    if (todo < n) {
+        RS_TRY(rs_pc_excite(h));
+        if (first_bad) *first_bad = todo;
+        RS_CHECK(false, RS_ERR_LUT_KEY, "path-integration LUT key outside the table at step %d "
+                 "(posecell_network.py:249)", todo);
+    }
     return RS_OK;
 }
 

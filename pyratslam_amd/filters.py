@@ -196,3 +196,35 @@ def batch_control(odometry, th, table):
     for o in np.unique(zorig):
         zf[zorig == o] = filter_1d(int(o))
     return (rx.astype(np.int32), ry.astype(np.int32), rows.astype(np.int32), zf, first_bad)
+
+
+ZORIG_MARGIN = 8
+
+
+def odometry_tables(th, table, margin=ZORIG_MARGIN):
+    """Tables of the library-side control (rs_pc_set_odometry_tables,
+    rs_pc_odom_control): every transcendental of path_integration evaluated by
+    NumPy exactly as step_control evaluates it, so the library applies only
+    correctly rounded IEEE operations to them.  Theta-filter origins cover
+    |origin| <= th // 2 + margin (|vrot| up to about pi + margin layers per step)."""
+    cos_a, sin_a = layer_trig(th)
+    zmin = -(th // 2 + margin)
+    nz = 2 * (th // 2 + margin) + 1
+    return dict(vtrans_scale=PC_CELL_X_SIZE, vrot_scale=2.0 * np.pi / th,
+                cos_a=np.ascontiguousarray(cos_a, dtype=np.float64),
+                sin_a=np.ascontiguousarray(sin_a, dtype=np.float64),
+                key_min=LUT_KEYS.start, nkeys=len(LUT_KEYS),
+                key_rows=np.ascontiguousarray(table._key_to_row, dtype=np.int32),
+                zorig_min=zmin, nz=nz,
+                zf_table=np.ascontiguousarray(
+                    np.stack([filter_1d(o) for o in range(zmin, zmin + nz)]), dtype=np.float64))
+
+
+def table_args(t):
+    """rs_pc_set_odometry_tables / rs_pc_odom_control table arguments as ctypes values."""
+    import ctypes
+    f64 = ctypes.POINTER(ctypes.c_double)
+    return (t['vtrans_scale'], t['vrot_scale'], t['cos_a'].ctypes.data_as(f64),
+            t['sin_a'].ctypes.data_as(f64), t['key_min'], t['nkeys'],
+            t['key_rows'].ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), t['zorig_min'], t['nz'],
+            t['zf_table'].ctypes.data_as(f64))

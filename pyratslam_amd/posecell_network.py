@@ -85,6 +85,15 @@ class PoseCellNetwork:
                                         ctypes.c_void_p)(('rs_pc_update', self._lib))
         self._out3 = np.empty(3, dtype=np.int32)
         self._out3_addr = self._out3.ctypes.data
+        self._upload_odometry_tables()
+        self._update_odom = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
+                                             ctypes.c_double, ctypes.c_void_p)(
+            ('rs_pc_update_odom', self._lib))
+
+    def _upload_odometry_tables(self):
+        """Tables for the library-side control of update()/run() (filters.odometry_tables)."""
+        self._odo_tables = F.odometry_tables(self.shape[2], self.filter_table)
+        _lib.check(self._lib.rs_pc_set_odometry_tables(self._h, *F.table_args(self._odo_tables)))
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
@@ -155,8 +164,30 @@ class PoseCellNetwork:
         return tuple(int(v) for v in out)
 
     def update(self, v=(0.0, 0.0)):
-        """One network step (posecell_network.py:326-353); returns and stores max_pc."""
+        """One network step (posecell_network.py:326-353); returns and stores max_pc.
+
+        One FFI call: the library derives path_integration's control from (vtrans,
+        vrot) bit-identically to filters.step_control (rs_pc_update_odom)."""
         vtrans, vrot = float(v[0]), float(v[1])
+        out = self._out3
+        with self._mutex:
+            st = self._update_odom(self._h, vtrans, vrot, self._out3_addr)
+            if st == _lib.RS_OK:
+                self.max_pc = (int(out[0]), int(out[1]), int(out[2]))
+                self._max_valid = True
+                return self.max_pc
+            if st == _lib.RS_ERR_LUT_KEY:
+                # steps 1-4 ran in the library; raise the reference's KeyError((k, k))
+                self._max_valid = False
+                F.step_control(vtrans, vrot, self.shape[2], self.filter_table)
+                raise KeyError('path-integration LUT miss')  # pragma: no cover
+            if st != _lib.RS_ERR_CTL_RANGE:
+                _lib.check(st)
+        return self._update_host_control(vtrans, vrot)
+
+    def _update_host_control(self, vtrans, vrot):
+        """update() with the control computed here in NumPy (filters.step_control) and
+        handed to rs_pc_update: for odometry outside the library's control tables."""
         try:
             ox, oy, rows, zf, _ = F.step_control(vtrans, vrot, self.shape[2], self.filter_table)
         except KeyError:
@@ -183,7 +214,32 @@ class PoseCellNetwork:
         Returns an int32 array (n, 3) of max_pc per step.  A LUT KeyError at step
         s leaves the state the reference would (steps < s done, then steps 1-4 of s).
         """
-        od = np.asarray(odometry, dtype=np.float64).reshape(-1, 2)
+        od = np.ascontiguousarray(np.asarray(odometry, dtype=np.float64).reshape(-1, 2))
+        n = od.shape[0]
+        out = np.empty((n, 3), dtype=np.int32)
+        bad = ctypes.c_int(-1)
+        with self._mutex:
+            st = self._lib.rs_pc_run_odom(self._h, n, _lib.ptr(od, ctypes.c_double),
+                                          _lib.ptr(out, ctypes.c_int32), ctypes.byref(bad))
+            if st in (_lib.RS_OK, _lib.RS_ERR_LUT_KEY):
+                todo = n if st == _lib.RS_OK else bad.value
+                if todo > 0:
+                    self.max_pc = tuple(int(v) for v in out[todo - 1])
+                    self._max_valid = True
+                if st == _lib.RS_ERR_LUT_KEY:
+                    self._max_valid = False
+            elif st != _lib.RS_ERR_CTL_RANGE:
+                _lib.check(st)
+        if st == _lib.RS_ERR_CTL_RANGE:
+            return self._run_host_control(od)
+        if st == _lib.RS_ERR_LUT_KEY:
+            F.step_control(od[bad.value, 0], od[bad.value, 1], self.shape[2], self.filter_table)
+            raise KeyError('LUT miss at step %d' % bad.value)  # pragma: no cover
+        return out
+
+    def _run_host_control(self, od):
+        """run() with the control computed here (filters.batch_control) and handed to
+        rs_pc_run: for odometry outside the library's control tables."""
         n = od.shape[0]
         ox, oy, rows, zf, first_bad = F.batch_control(od, self.shape[2], self.filter_table)
         todo = n if first_bad is None else first_bad

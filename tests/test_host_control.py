@@ -103,3 +103,77 @@ def test_view_mask_matches_reference(name):
     assert shape == tuple(d['shape'])
     m2, s2 = V.py2_mask((p[0], p[1]), (p[2], p[3]), p[4], p[5], p[6], p[7])
     assert np.array_equal(mask, m2) and shape == s2
+
+
+def _library_control(th, od):
+    """rs_pc_odom_control (host-only entry of libratslam_hip.so) over odometry od (n, 2)."""
+    import ctypes
+    from pyratslam_amd import _lib
+    lib = _lib.load()
+    t = F.odometry_tables(th, F.FilterTable())
+    od = np.ascontiguousarray(od, dtype=np.float64)
+    n = od.shape[0]
+    ox = np.empty((n, th), np.int32)
+    oy = np.empty((n, th), np.int32)
+    rows = np.empty((n, th), np.int32)
+    zf = np.empty((n, 7))
+    st = np.empty(n, np.int32)
+    _lib.check(lib.rs_pc_odom_control(th, *F.table_args(t), n, _lib.ptr(od, ctypes.c_double),
+                                      _lib.ptr(ox, ctypes.c_int32), _lib.ptr(oy, ctypes.c_int32),
+                                      _lib.ptr(rows, ctypes.c_int32), _lib.ptr(zf, ctypes.c_double),
+                                      _lib.ptr(st, ctypes.c_int32)))
+    return ox, oy, rows, zf, st
+
+
+def _edge_odometry(th, n, seed):
+    """Odometry whose per-layer residuals sit on the LUT key boundaries: vtrans chosen
+    so that vtrans/0.2 * cos(layer) lands within a few ulps of k/10 and of x.5."""
+    rng = np.random.default_rng(seed)
+    cos_a, _ = F.layer_trig(th)
+    layer = rng.integers(0, th, n)
+    c = cos_a[layer]
+    c[np.abs(c) < 1e-3] = 1.0
+    target = rng.integers(-30, 30, n) + rng.integers(-5, 6, n) / 10.0
+    vt = target / c * 0.2
+    vt += rng.integers(-4, 5, n) * np.spacing(np.abs(vt) + 1e-300)
+    vrot = (rng.integers(-th, th, n) + 0.5) * (2.0 * np.pi / th)
+    vrot += rng.integers(-2, 3, n) * np.spacing(np.abs(vrot))
+    return np.stack([vt, vrot], axis=1)
+
+
+@pytest.mark.parametrize('th', [18, 36, 72])
+def test_library_control_bit_identical_to_numpy(th):
+    """The library-side control (rs_pc_update_odom / rs_pc_run_odom) equals
+    filters.step_control bit for bit, including on key and rounding boundaries,
+    and reports the reference's KeyError (:249) / out-of-table origins."""
+    table = F.FilterTable()
+    rng = np.random.default_rng(th)
+    live = np.stack([rng.uniform(0, 0.6, 3000), rng.uniform(-0.15, 0.15, 3000)], axis=1)
+    wide = np.stack([rng.uniform(-3, 3, 3000), rng.uniform(-7, 7, 3000)], axis=1)
+    od = np.concatenate([live, wide, _edge_odometry(th, 6000, th),
+                         [[0.0, 0.0], [-0.0, -0.0], [np.nan, 0.0], [0.1, np.nan], [1e300, 0.0]]])
+    ox, oy, rows, zf, st = _library_control(th, od)
+    from pyratslam_amd import _lib
+    n_ok = n_key = n_range = 0
+    for i, (vt, vr) in enumerate(od):
+        try:
+            rx, ry, rr, zz, _ = F.step_control(float(vt), float(vr), th, table)
+        except (KeyError, ValueError, OverflowError) as e:
+            if isinstance(e, KeyError):
+                assert st[i] == _lib.RS_ERR_LUT_KEY, (i, vt, vr, st[i])
+                n_key += 1
+            else:   # math.floor(nan / inf): the library defers to the host path
+                assert st[i] == _lib.RS_ERR_CTL_RANGE, (i, vt, vr, st[i])
+                n_range += 1
+            continue
+        if st[i] == _lib.RS_ERR_CTL_RANGE:
+            n_range += 1
+            o = math.floor(float(vr) / (2.0 * np.pi / th) + .5)
+            assert abs(o) > th // 2 + F.ZORIG_MARGIN or abs(float(vt)) / 0.2 >= 2 ** 30
+            continue
+        assert st[i] == _lib.RS_OK, (i, vt, vr, st[i])
+        n_ok += 1
+        assert np.array_equal(ox[i], rx) and np.array_equal(oy[i], ry), (i, vt, vr)
+        assert np.array_equal(rows[i], rr), (i, vt, vr)
+        assert zf[i].tobytes() == zz.tobytes(), (i, vt, vr)
+    assert n_ok > 5000 and n_key > 100 and n_range > 0

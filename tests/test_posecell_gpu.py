@@ -228,3 +228,32 @@ def test_default_form_by_grid_size(pcn, monkeypatch):
     monkeypatch.setenv('RS_PC_FORM', 'stream:2,8,1,3')   # spills at float64: refused
     with pytest.raises(ValueError):
         pcn((64, 64, 36), precision='float64')
+
+
+@pytest.mark.parametrize('shape', [(32, 32, 18), (64, 64, 36)])
+def test_library_control_matches_host_control(pcn, shape):
+    """update()/run() take the odometry through rs_pc_update_odom / rs_pc_run_odom;
+    the state must be bit-identical to the NumPy-control path (rs_pc_update /
+    rs_pc_run), including odometry outside the library's tables (host fallback)."""
+    od = odometry(60, 11, vmax=1.2, rmax=0.4)
+    od[20] = (0.3, 6.0)      # theta origin outside the tables -> host control
+    od[40] = (0.25, -6.5)
+    a, b, c, d = (pcn(shape) for _ in range(4))
+    for n in (a, b, c, d):
+        n.inject(1, (shape[0] // 2, shape[1] // 2, shape[2] // 2))
+    ma = [a.update(v) for v in od]
+    mb = [b._update_host_control(float(v[0]), float(v[1])) for v in od]
+    mc = c.run(od)
+    md = d._run_host_control(np.ascontiguousarray(od))
+    assert ma == mb
+    assert np.array_equal(mc, md) and [tuple(r) for r in mc] == ma
+    pa = a.posecells
+    for n in (b, c, d):
+        assert n.posecells.tobytes() == pa.tobytes()
+    # a batch that needs the host fallback as a whole (step 20 is outside the tables)
+    e, f = pcn(shape), pcn(shape)
+    for n in (e, f):
+        n.inject(1, (shape[0] // 2, shape[1] // 2, shape[2] // 2))
+    assert np.array_equal(e.run(od[15:25]), f._run_host_control(np.ascontiguousarray(od[15:25])))
+    assert e.posecells.tobytes() == f.posecells.tobytes()
+    assert e.run(np.zeros((0, 2))).shape == (0, 3)
