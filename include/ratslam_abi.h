@@ -30,6 +30,7 @@
  *                   (scores = ViewTemplate.match  view_templates.py:16-28)
  *   rs_vt_match_batch  a loop of ViewTemplates.match calls (exact sequential
  *                   semantics incl. in-batch appends), or a frozen-library scan
+ *   rs_vt_match_stream  many frozen-library batches, one host synchronisation
  *   rs_vt_read      ViewTemplate.template         view_templates.py:11
  *   rs_vt_set_subsample / rs_vt_match_frames
  *                   input[self.mask].reshape(...) view_templates.py:48-57,64 (on device)
@@ -189,6 +190,14 @@ int rs_vt_read(rs_vt* h, int64_t index, uint8_t* out);
  * is_new[i]:     1 if query i was appended as a new template                 */
 int rs_vt_match_batch(rs_vt* h, int nq, const uint8_t* queries, int mode,
                       uint64_t* best_score, int64_t* best_index, uint8_t* is_new);
+/* nb batches of nq queries each against the frozen library (nb successive
+ * rs_vt_match_batch(RS_VT_FROZEN) calls), queued back to back on the device
+ * with one host synchronisation.  queries[nb*nq*H*W]: host memory, or device
+ * memory (rs_dev_malloc) whose batches the query-form kernels read in place.
+ * Sharded handles reduce each batch with the RCCL allreduce(min) on the same
+ * stream.  best_score / best_index[nb*nq] as in rs_vt_match_batch. */
+int rs_vt_match_stream(rs_vt* h, int nb, int nq, const uint8_t* queries, uint64_t* best_score,
+                       int64_t* best_index);
 /* single query, RS_VT_SEQUENTIAL semantics */
 int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* best_index,
                 int* is_new);

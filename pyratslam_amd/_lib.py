@@ -91,6 +91,7 @@ SIGNATURES = {
     'rs_vt_add': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, _i64p]),
     'rs_vt_read': (ctypes.c_int, [_vp, ctypes.c_int64, _u8p]),
     'rs_vt_match_batch': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int, _u64p, _i64p, _u8p]),
+    'rs_vt_match_stream': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _u64p, _i64p]),
     'rs_vt_match': (ctypes.c_int, [_vp, _u8p, _u64p, _i64p, _c_int_p]),
     'rs_vt_scores': (ctypes.c_int, [_vp, ctypes.c_int, _u8p, ctypes.c_int64, ctypes.c_int64, _u64p]),
     'rs_vt_set_subsample': (ctypes.c_int, [_vp, ctypes.c_int64, _i32p]),

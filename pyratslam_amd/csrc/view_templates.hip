@@ -631,31 +631,69 @@ __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __re
     }
 }
 
-// One block per query: query planes for every start row, and QS.
+// 8x8 bit-matrix transpose of 8 bytes held as (lo = bytes 0-3, hi = bytes 4-7):
+// bit c of byte r  ->  bit r of byte c (three delta swaps, Hacker's Delight 7-3).
+__device__ inline void transpose8x8(uint32_t& lo, uint32_t& hi) {
+    uint32_t t;
+    t = (lo ^ (lo >> 7)) & 0x00AA00AAu;   lo ^= t ^ (t << 7);
+    t = (hi ^ (hi >> 7)) & 0x00AA00AAu;   hi ^= t ^ (t << 7);
+    t = (lo ^ (lo >> 14)) & 0x0000CCCCu;  lo ^= t ^ (t << 14);
+    t = (hi ^ (hi >> 14)) & 0x0000CCCCu;  hi ^= t ^ (t << 14);
+    t = (lo ^ (hi << 4)) & 0xF0F0F0F0u;   lo ^= t;  hi ^= t >> 4;
+}
+
+// 4x4 byte transpose: out[k] byte q = byte k of in[q].
+__device__ inline void transpose4x4_bytes(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                          uint32_t (&o)[4]) {
+    // pairs: (a,b) -> byte k of a, byte k of b interleaved; likewise (c,d)
+    const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
+    const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
+    const uint32_t cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);  // c0 d0 c1 d1
+    const uint32_t cd_hi = __builtin_amdgcn_perm(d, c, 0x07030602u);  // c2 d2 c3 d3
+    o[0] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x05040100u);          // a0 b0 c0 d0
+    o[1] = __builtin_amdgcn_perm(cd_lo, ab_lo, 0x07060302u);          // a1 b1 c1 d1
+    o[2] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x05040100u);
+    o[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
+}
+
+// One block per query: query planes for every start row, and QS.  Phase 1: each
+// thread bit-transposes one 8-byte row segment (row r, column group cg) so byte
+// k holds bit k of its 8 pixels (rows outside [M, H-M) become zero), and adds
+// the segment to QS.  Phase 2: each thread assembles one unit (4 rows from start
+// row S0 + si, column group cg): plane k = byte k of its 4 segments, two 16-byte
+// stores.  Bit b of plane k = bit k of pixel (row + b/8, col 8cg + b%8).
 __global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restrict__ raw, int H,
                                                         int M, uint32_t* __restrict__ qp,
                                                         uint32_t* __restrict__ qsum) {
     constexpr int W = 8 * PL_CG;
     __shared__ uint32_t s_red[4];
+    __shared__ uint2 s_t[64 * W / 8];   // transposed segments (H <= 64)
     const int NS = H - 2 * M + 3, S0 = M - 3;
     const uint8_t* Q = raw + (size_t)blockIdx.x * H * W;
     uint32_t* out = qp + (size_t)blockIdx.x * PL_CG * NS * 8;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31;
-    for (int u0 = 2 * wave; u0 < PL_CG * NS; u0 += 8) {
-        const int u = u0 + (lane >> 5);
-        const int cg = u / NS, si = u - cg * NS, r = S0 + si + (i >> 3);
-        const uint32_t byte =
-            (u < PL_CG * NS && r >= M && r < H - M) ? Q[(size_t)r * W + 8 * cg + (i & 7)] : 0u;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const unsigned long long m = __ballot((byte >> k) & 1u);
-            if (i == k && u < PL_CG * NS) out[(size_t)u * 8 + k] = (uint32_t)(lane < 32 ? m : m >> 32);
-        }
-    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t part = 0;
-    const uint32_t* rows = reinterpret_cast<const uint32_t*>(Q + (size_t)M * W);
-    for (int d = threadIdx.x; d < (H - 2 * M) * W / 4; d += blockDim.x)
-        part = __builtin_amdgcn_sad_u8(rows[d], 0u, part);
+    for (int d = threadIdx.x; d < H * W / 8; d += blockDim.x) {
+        uint2 v = reinterpret_cast<const uint2*>(Q)[d];
+        const int r = d / (W / 8);
+        const bool live = r >= M && r < H - M;
+        if (live) part = __builtin_amdgcn_sad_u8(v.y, 0u, __builtin_amdgcn_sad_u8(v.x, 0u, part));
+        transpose8x8(v.x, v.y);
+        s_t[d] = live ? v : make_uint2(0u, 0u);
+    }
+    __syncthreads();
+    const int NU = PL_CG * NS;
+    for (int u = threadIdx.x; u < NU; u += blockDim.x) {
+        const int cg = u / NS, r0 = S0 + (u - cg * NS);
+        const uint2 q0 = s_t[(r0 + 0) * PL_CG + cg], q1 = s_t[(r0 + 1) * PL_CG + cg];
+        const uint2 q2 = s_t[(r0 + 2) * PL_CG + cg], q3 = s_t[(r0 + 3) * PL_CG + cg];
+        uint32_t lo[4], hi[4];
+        transpose4x4_bytes(q0.x, q1.x, q2.x, q3.x, lo);
+        transpose4x4_bytes(q0.y, q1.y, q2.y, q3.y, hi);
+        uint4* o = reinterpret_cast<uint4*>(out + (size_t)u * 8);
+        o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+        o[1] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
     if (lane == 0) s_red[wave] = part;
@@ -869,6 +907,9 @@ struct rs_vt {
     unsigned long long* dBest = nullptr;
     unsigned long long* hBest = nullptr;  // pinned
     unsigned long long* hBestDev = nullptr;  // hBest in the device's address space
+    unsigned long long* dStream = nullptr;   // keys of rs_vt_match_stream, one row per batch
+    unsigned long long* hStream = nullptr;   // pinned copy (nb * nq)
+    size_t streamCap = 0;
     int bestClean = 0;     // leading dBest entries known to hold UINT64_MAX
     int bestPending = 0;   // bestClean once the keys of the running scan are exported
     // index lists for stores
@@ -1056,16 +1097,20 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     return vt_build_forms(h, nq);
 }
 
-// Build the query forms of the nq raw queries already in dQraw.
-int vt_build_forms(rs_vt* h, int nq) {
-    hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H, h->W,
-                       h->WD, h->M, h->dQf, h->dQsum);
-    if (h->planar)
-        hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, h->dQraw, h->H,
+// Build the query forms of nq raw queries in device memory (default: dQraw).
+// The plane scan reads only the planes; the byte-SWAR forms serve the other scans.
+int vt_build_forms(rs_vt* h, int nq, const uint8_t* src) {
+    if (!h->planar)
+        hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, src, h->H, h->W,
+                           h->WD, h->M, h->dQf, h->dQsum);
+    else
+        hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, src, h->H,
                            h->M, h->dQp, h->dQsumRaw);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
+
+int vt_build_forms(rs_vt* h, int nq) { return vt_build_forms(h, nq, h->dQraw); }
 
 // Subsample nf frames on the device into the raw query buffer, then build the
 // forms.  Host frames go through a pinned staging buffer; device-resident frames
@@ -1378,6 +1423,70 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
     return RS_OK;
 }
 
+// nb frozen-library batches queued back to back with one host synchronisation:
+// per batch the forms are built straight from the raw queries (device-resident
+// ones in place; host ones through dQraw), the library is scanned into that
+// batch's row of keys, and the row is min-reduced over the ranks on the same
+// stream; one copy brings all rows back.
+int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint64_t* best_score,
+                         int64_t* best_index) {
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    RS_CHECK(nb >= 0 && nq >= 0, RS_ERR_ARG, "negative batch or query count");
+    if (nb == 0 || nq == 0) return RS_OK;
+    RS_CHECK(queries, RS_ERR_ARG, "null queries");
+    RS_CHECK(h->nranks == 1 || h->comm, RS_ERR_STATE, "sharded handle without a communicator: "
+             "rs_vt_match_stream needs the RCCL reduction (rs_vt_attach_comm)");
+    RS_HIP(hipSetDevice(h->device));
+    RS_TRY(vt_grow_queries(h, nq));
+    const size_t total = (size_t)nb * nq;
+    if (total > h->streamCap) {
+        if (h->hStream) RS_HIP(hipHostFree(h->hStream));
+        if (h->dStream) RS_HIP(hipFree(h->dStream));
+        h->hStream = h->dStream = nullptr;
+        h->streamCap = 0;
+        RS_HIP(hipHostMalloc(&h->hStream, sizeof(unsigned long long) * total, hipHostMallocDefault));
+        RS_HIP(hipMalloc(&h->dStream, sizeof(unsigned long long) * total));
+        h->streamCap = total;
+    }
+    hipPointerAttribute_t attr{};
+    const bool on_device = hipPointerGetAttributes(&attr, queries) == hipSuccess &&
+                           attr.type == hipMemoryTypeDevice;
+    (void)hipGetLastError();  // a host pointer is not an error
+    RS_CHECK(!on_device || reinterpret_cast<uintptr_t>(queries) % 8 == 0, RS_ERR_ARG,
+             "device-resident queries must be 8-byte aligned");
+    const size_t qb = (size_t)h->H * h->W * nq;
+    RS_HIP(hipMemsetAsync(h->dStream, 0xFF, sizeof(unsigned long long) * total, h->stream));
+    h->stagedQ = 0;  // the forms no longer match dQraw
+    h->timedScan = false;
+    const int64_t lc = local_count_of(h, h->count);
+    for (int b = 0; b < nb; ++b) {
+        unsigned long long* keys = h->dStream + (size_t)b * nq;
+        const ScanOut out{keys, nullptr, 0};
+        const uint8_t* src = queries + qb * b;
+        if (!on_device) {
+            RS_HIP(hipMemcpyAsync(h->dQraw, src, qb, hipMemcpyHostToDevice, h->stream));
+            src = h->dQraw;
+        }
+        RS_TRY(vt_build_forms(h, nq, src));
+        RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
+        if (h->nranks > 1) {
+            ncclResult_t r = ncclAllReduce(keys, keys, (size_t)nq, ncclUint64, ncclMin, h->comm,
+                                           h->stream);
+            RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
+                     ncclGetErrorString(r));
+        }
+    }
+    RS_HIP(hipMemcpyAsync(h->hStream, h->dStream, sizeof(unsigned long long) * total,
+                          hipMemcpyDeviceToHost, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    for (size_t i = 0; i < total; ++i) {
+        const unsigned long long k = h->hStream[i];
+        if (best_index) best_index[i] = k == NO_KEY ? -1 : (int64_t)(k & 0xFFFFFFFFull);
+        if (best_score) best_score[i] = k == NO_KEY ? UINT64_MAX : (k >> 32);
+    }
+    return RS_OK;
+}
+
 int vt_match_impl(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64_t* best_score,
                   int64_t* best_index, uint8_t* is_new, bool frames = false) {
     RS_CHECK(mode == RS_VT_FROZEN || mode == RS_VT_SEQUENTIAL, RS_ERR_ARG, "unknown mode %d", mode);
@@ -1471,6 +1580,8 @@ int rs_vt_destroy(rs_vt* h) {
                     (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
                     (void*)h->dQsumRaw, (void*)h->dCtr, (void*)h->dPix, (void*)h->dFrames})
         if (p) (void)hipFree(p);
+    if (h->hStream) (void)hipHostFree(h->hStream);
+    if (h->dStream) (void)hipFree(h->dStream);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat,
                     (void*)h->hFrames})
         if (p) (void)hipHostFree(p);
@@ -1537,6 +1648,12 @@ int rs_vt_match_batch(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64
                       int64_t* best_index, uint8_t* is_new) {
     rs::clear_error();
     return vt_match_impl(h, nq, queries, mode, best_score, best_index, is_new);
+}
+
+int rs_vt_match_stream(rs_vt* h, int nb, int nq, const uint8_t* queries, uint64_t* best_score,
+                       int64_t* best_index) {
+    rs::clear_error();
+    return vt_match_stream_impl(h, nb, nq, queries, best_score, best_index);
 }
 
 int rs_vt_match(rs_vt* h, const uint8_t* query, uint64_t* best_score, int64_t* best_index,

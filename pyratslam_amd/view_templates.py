@@ -189,6 +189,34 @@ class ViewTemplates:
                 self._record(q, pcs if pcs is not None else [(0, 0, 0)] * n, idx, new)
         return idx, score, new.astype(bool)
 
+    def match_stream(self, queries, nq=None):
+        """Frozen-library matching of many batches with one host synchronisation
+        (rs_vt_match_stream): ``queries`` is a uint8 (nb, nq, H, W) host array, or
+        ``(nb, nq, _lib.DeviceBuffer)`` for batches already in HBM.  Returns
+        ``(index, score)`` shaped (nb, nq); nothing is appended."""
+        if isinstance(queries, tuple):
+            nb, nq, buf = int(queries[0]), int(queries[1]), queries[2]
+            if nb * nq * self.shape[0] * self.shape[1] > buf.nbytes:
+                raise ValueError('%d x %d queries exceed the %d-byte device buffer'
+                                 % (nb, nq, buf.nbytes))
+            qptr, keep = buf.ptr, buf
+        else:
+            q = np.asarray(queries)
+            if q.ndim != 4:
+                raise ValueError('match_stream takes (nb, nq, H, W) queries, got %r' % (q.shape,))
+            nb = q.shape[0]
+            q = self._check_templates(q.reshape((-1,) + q.shape[2:])).reshape(q.shape)
+            nq = q.shape[1]
+            qptr, keep = ctypes.c_void_p(q.ctypes.data), q
+        idx = np.empty((nb, nq), dtype=np.int64)
+        score = np.empty((nb, nq), dtype=np.uint64)
+        with self._mutex:
+            _lib.check(self._lib.rs_vt_match_stream(self._h, nb, nq, qptr,
+                                                    _lib.ptr(score, ctypes.c_uint64),
+                                                    _lib.ptr(idx, ctypes.c_int64)))
+        del keep
+        return idx, score
+
     def match(self, input, pc_x, pc_y, pc_th):
         """Best template for a frame, or a new one (view_templates.py:63-75)."""
         t = self.subsample(input)

@@ -324,3 +324,42 @@ def test_untimed_scans(vtmod):
     idx, _, _ = lib.match_templates(queries[:50], mode=0)
     assert np.array_equal(idx, ref[:50].argmin(axis=1))
     assert lib.device_ms() > 0.0
+
+
+@pytest.mark.parametrize('t,nb,q', [(1000, 4, 256), (70, 3, 33), (0, 2, 5)])
+def test_match_stream_equals_frozen_batches(vtmod, t, nb, q):
+    """rs_vt_match_stream (nb batches, one host sync) == nb rs_vt_match_batch(FROZEN)
+    calls, from host memory and from batches resident in HBM; the oracle pins scores."""
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(max(t, 1), 64, 32, seed=t + 5)[:t]
+    batches = np.stack([V.synthetic_queries(V.synthetic_library(max(t, 8), 64, 32, seed=t + 5),
+                                            q, seed=100 + b)[0] for b in range(nb)])
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    if t:
+        lib.add(lib_np)
+    idx_h, score_h = lib.match_stream(batches)
+    buf = _lib.DeviceBuffer(batches.nbytes).upload(batches)
+    idx_d, score_d = lib.match_stream((nb, q, buf))
+    buf.close()
+    assert np.array_equal(idx_h, idx_d) and np.array_equal(score_h, score_d)
+    # the staged batch is gone after a stream (its forms came from elsewhere)
+    with pytest.raises(RuntimeError):
+        _lib.check(lib._lib.rs_vt_match_batch(lib._h, q, None, 0, None, None, None))
+    for b in range(nb):
+        idx, score, new = lib.match_templates(batches[b], mode=0)
+        assert not new.any()
+        assert np.array_equal(idx_h[b], idx) and np.array_equal(score_h[b], score)
+        for i in range(0, q, max(1, q // 8)):
+            if t == 0:
+                assert idx_h[b, i] == -1 and score_h[b, i] == np.iinfo(np.uint64).max
+                continue
+            ref = V.vt_scores_library(lib_np, batches[b, i])
+            assert score_h[b, i] == ref.min() and idx_h[b, i] == int(np.argmin(ref))
+    assert lib.count() == t
+
+
+def test_match_stream_refuses_host_reduced_shards(vtmod):
+    s = vtmod.ShardedViewTemplates.from_shape((64, 32), 45000, 0, 2, reducer=lambda k: k)
+    s.add(V.synthetic_library(10, 64, 32, seed=3))
+    with pytest.raises(RuntimeError):
+        s.match_stream(np.zeros((1, 4, 64, 32), np.uint8))
