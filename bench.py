@@ -57,12 +57,13 @@ def parse():
                     help='configs[2]: fixed library sharded over the ranks (strong scaling); 0 = off')
     ap.add_argument('--library-steps', type=int, default=5)
     ap.add_argument('--pc-shape', default='64,64,36')
-    ap.add_argument('--pc-steps', type=int, default=2000, help='timed pose-cell steps')
+    ap.add_argument('--pc-steps', type=int, default=10000,
+                    help='timed pose-cell steps (SURVEY.md 8(d): >= 10,000)')
     ap.add_argument('--pc-warmup', type=int, default=200)
-    ap.add_argument('--pc-calls', type=int, default=1000, help='timed per-call update()s')
+    ap.add_argument('--pc-calls', type=int, default=10000, help='timed per-call update()s')
     ap.add_argument('--pc-stress-shape', default='128,128,72',
                     help='configs[3] stencil-stress grid, reported beside the headline grid')
-    ap.add_argument('--pc-stress-steps', type=int, default=400)
+    ap.add_argument('--pc-stress-steps', type=int, default=10000)
     ap.add_argument('--no-pc-stress', action='store_true')
     ap.add_argument('--replay-messages', type=int, default=600,
                     help='configs[4] replay: odometry messages (each followed by a frame)')
