@@ -907,6 +907,8 @@ struct rs_vt {
     unsigned long long* dBest = nullptr;
     unsigned long long* hBest = nullptr;  // pinned
     unsigned long long* hBestDev = nullptr;  // hBest in the device's address space
+    hipStream_t cstream = nullptr;           // rs_vt_match_stream's collective stream
+    hipEvent_t evScan = nullptr, evComm = nullptr;
     unsigned long long* dStream = nullptr;   // keys of rs_vt_match_stream, one row per batch
     unsigned long long* hStream = nullptr;   // pinned copy (nb * nq)
     size_t streamCap = 0;
@@ -1425,9 +1427,9 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
 
 // nb frozen-library batches queued back to back with one host synchronisation:
 // per batch the forms are built straight from the raw queries (device-resident
-// ones in place; host ones through dQraw), the library is scanned into that
-// batch's row of keys, and the row is min-reduced over the ranks on the same
-// stream; one copy brings all rows back.
+// ones in place; host ones through dQraw) and the library is scanned into that
+// batch's row of keys; with a communicator the row is min-reduced over the ranks
+// on a second stream, overlapped with the next batch; one copy brings all rows back.
 int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint64_t* best_score,
                          int64_t* best_index) {
     RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
@@ -1436,6 +1438,11 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     RS_CHECK(queries, RS_ERR_ARG, "null queries");
     RS_CHECK(h->nranks == 1 || h->comm, RS_ERR_STATE, "sharded handle without a communicator: "
              "rs_vt_match_stream needs the RCCL reduction (rs_vt_attach_comm)");
+    if (h->comm && !h->cstream) {
+        RS_HIP(hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking));
+        RS_HIP(hipEventCreateWithFlags(&h->evScan, hipEventDisableTiming));
+        RS_HIP(hipEventCreateWithFlags(&h->evComm, hipEventDisableTiming));
+    }
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(vt_grow_queries(h, nq));
     const size_t total = (size_t)nb * nq;
@@ -1469,12 +1476,20 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
         }
         RS_TRY(vt_build_forms(h, nq, src));
         RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
-        if (h->nranks > 1) {
+        if (h->comm) {
+            // the batch's row is reduced on the collective stream while the next
+            // batch's planes and scan run on the main stream (rows are distinct)
+            RS_HIP(hipEventRecord(h->evScan, h->stream));
+            RS_HIP(hipStreamWaitEvent(h->cstream, h->evScan, 0));
             ncclResult_t r = ncclAllReduce(keys, keys, (size_t)nq, ncclUint64, ncclMin, h->comm,
-                                           h->stream);
+                                           h->cstream);
             RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
                      ncclGetErrorString(r));
         }
+    }
+    if (h->comm) {
+        RS_HIP(hipEventRecord(h->evComm, h->cstream));
+        RS_HIP(hipStreamWaitEvent(h->stream, h->evComm, 0));
     }
     RS_HIP(hipMemcpyAsync(h->hStream, h->dStream, sizeof(unsigned long long) * total,
                           hipMemcpyDeviceToHost, h->stream));
@@ -1574,6 +1589,7 @@ int rs_vt_destroy(rs_vt* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
@@ -1587,6 +1603,9 @@ int rs_vt_destroy(rs_vt* h) {
         if (p) (void)hipHostFree(p);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->evScan) (void)hipEventDestroy(h->evScan);
+    if (h->evComm) (void)hipEventDestroy(h->evComm);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return RS_OK;
@@ -1800,7 +1819,7 @@ int rs_vt_attach_comm(rs_vt* h, int rank, int nranks, const uint8_t id[RS_UNIQUE
     RS_CHECK(h->count == 0 && h->comm == nullptr, RS_ERR_STATE,
              "attach the communicator before adding templates, once");
     RS_HIP(hipSetDevice(h->device));
-    if (nranks > 1) {
+    {  // also for nranks == 1: rs_vt_match_stream then runs its collective path
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         ncclComm_t comm = nullptr;  // kept only on success: destroy never sees a failed init

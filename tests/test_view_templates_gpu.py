@@ -363,3 +363,25 @@ def test_match_stream_refuses_host_reduced_shards(vtmod):
     s.add(V.synthetic_library(10, 64, 32, seed=3))
     with pytest.raises(RuntimeError):
         s.match_stream(np.zeros((1, 4, 64, 32), np.uint8))
+
+
+def test_match_stream_collective_path_one_rank(vtmod):
+    """A 1-rank RCCL communicator runs rs_vt_match_stream's collective path on one
+    GPU (each batch's allreduce on the second stream, overlapped with the next
+    batch, then joined): results equal the plain frozen matching."""
+    lib_np = V.synthetic_library(700, 64, 32, seed=9)
+    batches = np.stack([V.synthetic_queries(lib_np, 300, seed=40 + b)[0] for b in range(6)])
+    uid = vtmod.ShardedViewTemplates.unique_id()
+    s = vtmod.ShardedViewTemplates.from_shape((64, 32), 45000, 0, 1, reducer='rccl', unique_id=uid)
+    plain = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    s.add(lib_np)
+    plain.add(lib_np)
+    for _ in range(2):   # twice: the streams and events are reused
+        idx, score = s.match_stream(batches)
+        ref_idx, ref_score = plain.match_stream(batches)
+        assert np.array_equal(idx, ref_idx) and np.array_equal(score, ref_score)
+    for b in range(6):
+        i, sc, _ = plain.match_templates(batches[b], mode=0)
+        assert np.array_equal(idx[b], i) and np.array_equal(score[b], sc)
+    s.close()
+    plain.close()
