@@ -489,32 +489,17 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     static_assert(NR % NW == 0 && HK == NW && BK * BX == NW, "row tile / wave mapping");
     __shared__ T s_win[NR * RW];
     __shared__ T s_r[HK * BX * YP];
-    __shared__ T s_ftab[RT_NFMAX * FT];
-    __shared__ T s_f[HK * FT];
     __shared__ int s_row[NR];
     __shared__ int s_L[HK], s_ox[HK], s_oy[HK], s_fi[HK];
-    __shared__ T s_zf[FL];
     __shared__ double s_red[NW];
     __shared__ T s_bv[NW];
     __shared__ unsigned s_bl[NW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    (void)nf;  // filter indices are validated on the host (pc_check_ctl)
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(1, 0);
 
-    // issue everything that does not depend on the control: normalisation partials
-    // (reduced only at the end), the filter table, the theta filter
-    double pt[NPP];
-#pragma unroll
-    for (int u = 0; u < NPP; ++u) {
-        const int i = tid + u * RT_NT;
-        pt[u] = i < npart ? part[i] : 0.0;
-    }
-    double pextra = 0.0;  // npart beyond NPP * RT_NT (huge grids)
-    for (int i = tid + NPP * RT_NT; i < npart; i += RT_NT) pextra += part[i];
-    const bool whole_table = nf <= RT_NFMAX;
-    if (whole_table)
-        for (int idx = tid; idx < nf * FT; idx += RT_NT) s_ftab[idx] = filt[idx];
-    if (tid >= 64 && tid < 64 + FL) s_zf[tid - 64] = (T)ctl_zf(ctl, tid - 64);
     if (tid < HK) {
         const int L = rs::wrapi(k0 - HALF + tid, TH);
         s_L[tid] = L;
@@ -528,11 +513,6 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
         const int kk = tid / HX, a = tid - kk * HX;
         s_row[tid] = s_L[kk] * X + rs::wrapi(i0 - HALF + a + s_ox[kk], X);
     }
-    if (!whole_table)
-        for (int idx = tid; idx < HK * FT; idx += RT_NT) {
-            const int kk = idx / FT;
-            s_f[idx] = filt[s_fi[kk] * FT + idx - kk * FT];
-        }
     __syncthreads();
     PC_STAMP(1, 2);
 
@@ -544,6 +524,23 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) v[q][jc] = src[min(lane + 64 * jc, Y - 1)];
     }
+    // this wave's layer filter and the normalisation partials (reduced only at the
+    // end), issued behind the window loads: a barrier waits for every load in
+    // flight, so nothing global is loaded before the control barriers above
+    T f[FT];
+    {
+        const T* fsrc = filt + (size_t)s_fi[wave] * FT;
+#pragma unroll
+        for (int t = 0; t < FT; ++t) f[t] = fsrc[t];
+    }
+    double pt[NPP];
+#pragma unroll
+    for (int u = 0; u < NPP; ++u) {
+        const int i = tid + u * RT_NT;
+        pt[u] = i < npart ? part[i] : 0.0;
+    }
+    double pextra = 0.0;  // npart beyond NPP * RT_NT (huge grids)
+    for (int i = tid + NPP * RT_NT; i < npart; i += RT_NT) pextra += part[i];
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
         const int row = wave + NW * q;
@@ -566,10 +563,6 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     // 7x7 per-layer correlation (:273-274), register-blocked over the BX rows, clamp (:300)
     {
         const int kk = wave;
-        const T* fsrc = whole_table ? s_ftab + s_fi[kk] * FT : s_f + kk * FT;
-        T f[FT];
-#pragma unroll
-        for (int t = 0; t < FT; ++t) f[t] = fsrc[t];
 #pragma unroll
         for (int jc = 0; jc < JC; ++jc) {
             const int j = lane + 64 * jc;
@@ -616,7 +609,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 if (j >= Y) continue;
                 T acc = 0;
 #pragma unroll
-                for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * s_zf[z];
+                for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * (T)ctl_zf(ctl, z);
                 T val = acc > T(0) ? acc : T(0);
                 if (tot != 0.0) val = val / tt;
                 P[((size_t)gk * X + gi) * Y + j] = val;
