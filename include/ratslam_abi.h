@@ -149,7 +149,9 @@ int rs_pc_read(rs_pc* h, double* host_xyth);
 int rs_pc_write(rs_pc* h, const double* host_xyth);
 /* sum of all cells (float64 accumulation) */
 int rs_pc_total(rs_pc* h, double* total);
-/* device time of the last rs_pc_run/rs_pc_update, milliseconds (HIP events) */
+/* device time of the last rs_pc_run/rs_pc_update, milliseconds (HIP events around
+ * the step's launches; recorded only while profiling is enabled, else 0 -- the two
+ * event records cost about 1.5 us of a 31 us update() call) */
 int rs_pc_last_ms(rs_pc* h, double* ms);
 /* HIP-event time of each kernel of the last rs_pc_run, summed over its steps:
  * ms[0] = excitation kernel, ms[1] = path-integration kernel (events recorded

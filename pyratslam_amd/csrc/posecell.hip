@@ -1796,7 +1796,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                               h->stream));
     }
     if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
-    RS_HIP(hipEventRecord(h->ev0, h->stream));
+    if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
     for (int s = 0; s < n; ++s) {
         const int pb = h->profiling ? 4 * s : -1;
         if (inline_ctl) {
@@ -1822,9 +1822,10 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     hipLaunchKernelGGL(pc_res_export, dim3((n + 63) / 64 < 64 ? (n + 63) / 64 : 64), dim3(64), 0,
                        h->stream, h->dRes, n, h->hResDev);
     RS_HIP(hipGetLastError());
-    RS_HIP(hipEventRecord(h->ev1, h->stream));
+    if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
-    RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    if (h->profiling) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    else h->lastMs = 0.f;  // the step-bracketing events are recorded only while profiling
     if (h->profiling) {
         h->kernelMs[0] = h->kernelMs[1] = 0.0;
         for (int s = 0; s < n; ++s) {

@@ -261,7 +261,8 @@ class PoseCellNetwork:
         return out
 
     def device_ms(self):
-        """Device time (HIP events) of the last update/run, in ms."""
+        """Device time (HIP events) of the last update/run, in ms; recorded only while
+        profiling is enabled (``set_profiling``), else 0."""
         ms = ctypes.c_double()
         _lib.check(self._lib.rs_pc_last_ms(self._h, ctypes.byref(ms)))
         return ms.value

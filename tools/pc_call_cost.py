@@ -34,7 +34,7 @@ def main():
         net.update(v)
     t_upd = (time.perf_counter() - t) / n
     print({'step_control_us': 1e6 * t_ctl, 'rs_pc_update_us': 1e6 * t_call,
-           'update_us': 1e6 * t_upd, 'device_ms_last': net.device_ms()}, flush=True)
+           'update_us': 1e6 * t_upd}, flush=True)
     net.close()
 
 
