@@ -909,6 +909,9 @@ struct rs_vt {
     unsigned long long* hBestDev = nullptr;  // hBest in the device's address space
     hipStream_t cstream = nullptr;           // rs_vt_match_stream's collective stream
     hipEvent_t evScan = nullptr, evComm = nullptr;
+    uint32_t* dQpStream = nullptr;           // rs_vt_match_stream: every batch's query planes
+    uint32_t* dQsumStream = nullptr;
+    size_t qpStreamCap = 0;                  // queries
     unsigned long long* dStream = nullptr;   // keys of rs_vt_match_stream, one row per batch
     unsigned long long* hStream = nullptr;   // pinned copy (nb * nq)
     size_t streamCap = 0;
@@ -1466,15 +1469,46 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     h->stagedQ = 0;  // the forms no longer match dQraw
     h->timedScan = false;
     const int64_t lc = local_count_of(h, h->count);
+    // Device-resident batches of the plane scan: one launch builds every batch's
+    // planes (nb * nq blocks), then the scans run back to back, each pointed at
+    // its batch's slice.
+    const bool allplanes = on_device && h->planar && nb > 1;
+    const size_t qpq = (size_t)PL_CG * plane_ns(h) * 8;  // plane dwords per query
+    struct PlaneBufRestore {  // h->dQp / dQsumRaw point at the per-batch buffers on return
+        rs_vt* h;
+        uint32_t* p;
+        uint32_t* q;
+        ~PlaneBufRestore() { h->dQp = p; h->dQsumRaw = q; }
+    } restore{h, h->dQp, h->dQsumRaw};
+    if (allplanes) {
+        if (total > h->qpStreamCap) {
+            if (h->dQpStream) RS_HIP(hipFree(h->dQpStream));
+            if (h->dQsumStream) RS_HIP(hipFree(h->dQsumStream));
+            h->dQpStream = h->dQsumStream = nullptr;
+            h->qpStreamCap = 0;
+            RS_HIP(hipMalloc(&h->dQpStream, sizeof(uint32_t) * qpq * total));
+            RS_HIP(hipMalloc(&h->dQsumStream, sizeof(uint32_t) * total));
+            h->qpStreamCap = total;
+        }
+        RS_CHECK(total <= INT32_MAX, RS_ERR_ARG, "too many queries in one stream");
+        h->dQp = h->dQpStream;
+        h->dQsumRaw = h->dQsumStream;
+        RS_TRY(vt_build_forms(h, (int)total, queries));
+    }
     for (int b = 0; b < nb; ++b) {
         unsigned long long* keys = h->dStream + (size_t)b * nq;
         const ScanOut out{keys, nullptr, 0};
         const uint8_t* src = queries + qb * b;
-        if (!on_device) {
-            RS_HIP(hipMemcpyAsync(h->dQraw, src, qb, hipMemcpyHostToDevice, h->stream));
-            src = h->dQraw;
+        if (allplanes) {
+            h->dQp = h->dQpStream + qpq * nq * b;  // launch arguments are captured at enqueue
+            h->dQsumRaw = h->dQsumStream + (size_t)nq * b;
+        } else {
+            if (!on_device) {
+                RS_HIP(hipMemcpyAsync(h->dQraw, src, qb, hipMemcpyHostToDevice, h->stream));
+                src = h->dQraw;
+            }
+            RS_TRY(vt_build_forms(h, nq, src));
         }
-        RS_TRY(vt_build_forms(h, nq, src));
         RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
         if (h->comm) {
             // the batch's row is reduced on the collective stream while the next
@@ -1598,6 +1632,8 @@ int rs_vt_destroy(rs_vt* h) {
         if (p) (void)hipFree(p);
     if (h->hStream) (void)hipHostFree(h->hStream);
     if (h->dStream) (void)hipFree(h->dStream);
+    if (h->dQpStream) (void)hipFree(h->dQpStream);
+    if (h->dQsumStream) (void)hipFree(h->dQsumStream);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat,
                     (void*)h->hFrames})
         if (p) (void)hipHostFree(p);
