@@ -580,7 +580,10 @@ constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
     do {               \
     } while (0)
 #endif
-constexpr int PL_NB = 2;       // queries per LDS batch (staged planes; one reducing wave each)
+#ifndef PL_NB_Q
+#define PL_NB_Q 2
+#endif
+constexpr int PL_NB = PL_NB_Q;  // queries per LDS batch (staged planes; one reducing wave each)
 
 __device__ inline uint32_t plane_borrows(const uint32_t (&t)[8], const uint32_t* q) {
     uint32_t b = __builtin_amdgcn_bitop3_b32(t[0], q[0], 0u, 0x8E);
