@@ -2,31 +2,36 @@
 """Benchmark of the pyratslam hot path on MI355X (BASELINE.json metric).
 
 One JSON line on rank 0:
-  value        template compares/s of the whole job (all ranks): each step
-               matches a batch of `--queries` subsampled 64x32 uint8 views,
-               resident in HBM, against the whole library (`--templates-per-gpu`
-               per rank, sharded round-robin, first-argmin combined by one RCCL
-               allreduce(min, uint64) per batch).  Weak scaling: the library
-               grows with the number of GPUs.
+  value        template compares/s of the whole job (all ranks).  A step is one
+               ``rs_vt_match_stream`` call over `--batches-per-step` distinct
+               batches of `--queries` subsampled 64x32 uint8 views, resident in
+               HBM, matched against the whole library (`--templates-per-gpu` per
+               rank, sharded round-robin, first argmin combined by one RCCL
+               allreduce(min, uint64) per batch); results reach the host inside
+               the step.  Weak scaling: the library grows with the GPUs.
   library_sharded  configs[2]: a fixed 100k-template library sharded over the
-               ranks (strong scaling), same query batches and allreduce.
+               ranks (strong scaling), same batches and allreduce.
   pose_cell    64x64x36 pose-cell network steps/s (the other half of the
-               metric): batched `run()` (per-step control uploaded with the
-               odometry) and the per-call `update()` drop-in rate; replicated
-               per GPU (one network, nothing to shard).
-  roofline     dominant kernel = the template scan: SURVEY.md section 8(d)'s
-               2,048 algorithmic bytes per compare x compares per launch / the
-               scan kernel's average HIP-event duration; the pose-cell kernels'
-               roofline is in pose_cell.roofline (24 bytes per cell per step).
-  cpu_baseline the oracle (NumPy restatement of the reference) on this host's
-               cores, bounded sample, rank 0 at N=1.
+               metric): batched `run()` and the per-call `update()` drop-in
+               rate; replicated per GPU (one network, nothing to shard).
+  pose_cell_stress  configs[3]: the 128x128x72 grid plus its 10k-template scan.
+  roofline     dominant kernel = the template scan, which is bound by VALU issue
+               (each template is read once per launch and reused from registers
+               by every query): PMC VALU wave-instructions per launch / the scan
+               kernel's live HIP-event duration / the wave64 issue peak, with the
+               measured HBM bytes beside it (profiles/pmc_traffic.json).
+  cpu_baseline the oracle (C/OpenMP restatement of the reference) on this
+               host's cores, bounded sample, rank 0 at N=1.
 
-Usage: python bench.py [--gpus N --steps K --warmup W]; N>1 under
-torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE env).
+Usage: python bench.py [--gpus N --steps K --warmup W].  N > 1 launches its own
+N rank processes (pyratslam_amd.launch) unless a launcher such as
+torch.distributed.run already set RANK / WORLD_SIZE; the control plane is
+pyratslam_amd.dist (TCP, no PyTorch), the data path RCCL.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -35,27 +40,33 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from pyratslam_amd import launch  # noqa: E402
+from pyratslam_amd.dist import Dist  # noqa: E402,F401  (tests import bench.Dist)
+
+# wave64 VALU issue peak: one wave-instruction per 2 cycles per SIMD, 1,024 SIMDs,
+# 2.4 GHz (MI355X_MICROARCH.md chip table)
 VALU_PEAK_GINSTS = 1024 * 2.4 * 0.5
-SCAN_KERNELS = {'plane': 'vt_scan_plane_kernel', 'carry': 'vt_scan_carry_kernel',
-                'sad': 'vt_scan_lane_kernel', 'rb2': 'vt_scan_rb_kernel', 'rb3': 'vt_scan_rb_kernel',
-                'generic': 'vt_scan_generic_kernel'}
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_COMPARE = 64 * 32  # one stored 64x32 u8 template
-from pyratslam_amd.dist import Dist  # noqa: E402
-
+SCAN_KERNELS = {'plane': 'vt_scan_plane_kernel', 'carry': 'vt_scan_carry_kernel',
+                'generic': 'vt_scan_generic_kernel'}
 METRIC = 'pose-cell steps/sec (64×64×36) + template-compares/sec at 1/2/4/8 GPU'
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20, help='timed template batches')
+    ap.add_argument('--steps', type=int, default=20, help='timed steps (template match calls)')
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--queries', type=int, default=1024)
+    ap.add_argument('--batches-per-step', type=int, default=10,
+                    help='query batches matched per step (one rs_vt_match_stream call)')
+    ap.add_argument('--queries', type=int, default=1024, help='queries per batch (one scan launch)')
     ap.add_argument('--templates-per-gpu', type=int, default=1000)
     ap.add_argument('--library-total', type=int, default=100000,
                     help='configs[2]: fixed library sharded over the ranks (strong scaling); 0 = off')
-    ap.add_argument('--library-steps', type=int, default=5)
+    ap.add_argument('--library-steps', type=int, default=4)
+    ap.add_argument('--stress-templates', type=int, default=10000,
+                    help='configs[3]: templates per GPU scanned beside the stress grid; 0 = off')
     ap.add_argument('--pc-shape', default='64,64,36')
     ap.add_argument('--pc-steps', type=int, default=10000,
                     help='timed pose-cell steps (SURVEY.md 8(d): >= 10,000)')
@@ -75,55 +86,58 @@ def parse():
     return ap.parse_args()
 
 
-def bench_templates(args, d, total=None, steps=None, warmup=None):
-    """Frozen-library template matching.  Default (configs[1]): `--templates-per-gpu`
-    templates on every rank (weak scaling).  With `total` (configs[2]): a fixed
-    library of `total` templates sharded over the ranks (strong scaling)."""
-    from pyratslam_amd import _lib, synthetic
+def _sharded_library(args, d, T):
+    """(view-template handle with room for T local templates, reduce kind)."""
     from pyratslam_amd.view_templates import ShardedViewTemplates, ViewTemplates
+    n = d.world
+    if n == 1:
+        return ViewTemplates._from_shape((64, 32), 45000, device=d.dev, capacity=T), 'none'
+    if args.same_device:  # RCCL refuses two ranks on one GPU: host reducer
+        return (ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
+                                                device=d.dev, capacity=T), 'host-tcp-min')
+    uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
+    try:
+        return (ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer='rccl',
+                                                unique_id=uid, device=d.dev, capacity=T),
+                'rccl-allreduce-min-u64')
+    except Exception as e:  # pragma: no cover - recorded in the output, not hidden
+        print('rank %d: RCCL attach failed (%s); host reduction' % (d.rank, e), file=sys.stderr)
+        return (ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
+                                                device=d.dev, capacity=T), 'host-tcp-min')
+
+
+def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, bps=None):
+    """Frozen-library template matching.  ``per_gpu`` templates on every rank
+    (weak scaling), or a fixed library of ``total`` sharded over the ranks
+    (strong scaling).  A step = one rs_vt_match_stream call over ``bps``
+    distinct HBM-resident batches of ``args.queries`` queries."""
+    import ctypes
+
+    from pyratslam_amd import _lib, synthetic
     Q, n = args.queries, d.world
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
+    bps = args.batches_per_step if bps is None else bps
     if total is None:
-        T, total = args.templates_per_gpu, args.templates_per_gpu * n
+        T, total = per_gpu, per_gpu * n
     else:
         T = (total + n - 1) // n             # rank r holds templates g % n == r
-    reduce_kind = 'none'
-    if n == 1:
-        vts = ViewTemplates._from_shape((64, 32), 45000, device=d.dev, capacity=T)
-    elif args.same_device:  # RCCL refuses two ranks on one GPU: host reducer
-        vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
-                                              device=d.dev, capacity=T)
-        reduce_kind = 'gloo-host-min'
-    else:
-        uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
-        try:
-            vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer='rccl',
-                                                  unique_id=uid, device=d.dev, capacity=T)
-            reduce_kind = 'rccl-allreduce-min-u64'
-        except Exception as e:  # pragma: no cover - recorded, not hidden
-            print('rank %d: RCCL attach failed (%s); host gloo reduction' % (d.rank, e),
-                  file=sys.stderr)
-            vts = ShardedViewTemplates.from_shape((64, 32), 45000, d.rank, n, reducer=d.min_keys,
-                                                  device=d.dev, capacity=T)
-            reduce_kind = 'gloo-host-min'
+    vts, reduce_kind = _sharded_library(args, d, T)
     # every rank adds the whole global library; rank r keeps templates g % n == r
     for lo in range(0, total, 8192):
         vts.add(synthetic.library(min(8192, total - lo), seed=1, first=lo))
     qlib = synthetic.library(min(total, 4096), seed=1)
     queries, src = synthetic.queries(qlib, Q, seed=2)
     lib = vts._lib
-    import ctypes
     idx = np.empty(Q, dtype=np.int64)
     score = np.empty(Q, dtype=np.uint64)
     new = np.empty(Q, dtype=np.uint8)
-
-    # result pointers converted once (the arrays are reused every batch)
     p_score, p_idx, p_new = (_lib.ptr(score, ctypes.c_uint64), _lib.ptr(idx, ctypes.c_int64),
                              _lib.ptr(new, ctypes.c_uint8))
     p_queries = _lib.ptr(queries, ctypes.c_uint8)
 
     def match(staged):
+        """one batch through rs_vt_match_batch (or scan_local + host reduce + resolve)"""
         qp = None if staged else p_queries
         if vts.nranks > 1 and vts.reducer != 'rccl':
             local = np.empty(Q, dtype=np.uint64)
@@ -134,79 +148,97 @@ def bench_templates(args, d, total=None, steps=None, warmup=None):
         else:
             _lib.check(lib.rs_vt_match_batch(vts._h, Q, qp, _lib.RS_VT_FROZEN, p_score, p_idx, p_new))
 
-    match(staged=False)                      # stage the batch in HBM (+ correctness probe)
+    match(staged=False)                      # stage one batch (+ correctness probe)
     hits = src >= 0
     correct = bool(np.all(idx[hits] == src[hits]))
 
-    # Timed region: `steps` distinct query batches, resident in HBM before it starts,
-    # matched by one rs_vt_match_stream call (per batch: query forms, scan, RCCL
-    # min-allreduce when sharded, key export; one host sync at the end).  Handles
-    # reduced on the host (--same-device) run the per-batch loop instead.
+    # Distinct batches resident in HBM before the timed region (at most 400; longer
+    # runs cycle through them).  Handles reduced on the host (--same-device) run the
+    # per-batch loop instead of the stream.
     pipeline = 'stream' if (vts.nranks == 1 or vts.reducer == 'rccl') else 'per-batch'
-    sbufs, srcs = None, None
+    nres = max(1, min(steps * bps, 400))
+    nres -= nres % bps if nres >= bps else 0
+    bufs, srcs = None, None
     if pipeline == 'stream':
-        qs = [queries] + [synthetic.queries(qlib, Q, seed=2 + 1000 * b)[0] for b in range(1, steps)]
-        srcs = [src] + [synthetic.queries(qlib, Q, seed=2 + 1000 * b)[1] for b in range(1, steps)]
-        sbufs = _lib.DeviceBuffer(Q * queries[0].nbytes * steps, device=d.dev).upload(np.stack(qs))
+        qs, srcs = [queries], [src]
+        for b in range(1, nres):
+            q_, s_ = synthetic.queries_fast(qlib, Q, seed=2 + 1000 * b)
+            qs.append(q_)
+            srcs.append(s_)
+        bufs = _lib.DeviceBuffer(Q * queries[0].nbytes * nres, device=d.dev).upload(np.stack(qs))
         del qs
+        nchunk = max(1, nres // bps)
+        bpc = min(bps, nres)
+
+        def step(i):
+            c = i % nchunk
+            dev_ptr = bufs.offset(c * bpc * Q * queries[0].nbytes)
+            return vts.match_stream((bpc, Q, dev_ptr)), c
         try:
-            # warm-up: untimed passes over the same batches (the first sizes the
-            # stream's key buffers, which must not be allocated in the timed region)
-            for _ in range(max(1, (warmup + steps - 1) // steps)):
-                sidx, _ = vts.match_stream((steps, Q, sbufs))
-            correct = correct and bool(np.all(sidx[0][hits] == src[hits]))
+            for i in range(max(1, warmup)):          # the first sizes the stream's buffers
+                (sidx, _), c = step(i)
+                correct = correct and all(bool(np.all(sidx[b][srcs[c * bpc + b] >= 0] ==
+                                                      srcs[c * bpc + b][srcs[c * bpc + b] >= 0]))
+                                          for b in range(bpc))
         except Exception as e:  # pragma: no cover - recorded, not hidden
             print('rank %d: rs_vt_match_stream failed (%s); per-batch loop' % (d.rank, e),
                   file=sys.stderr)
             pipeline = 'per-batch'
-            sbufs.close()
-            sbufs = None
+            bufs.close()
+            bufs = None
             match(staged=False)
     if pipeline == 'per-batch':
+        bpc = 1
         for _ in range(warmup):
             match(staged=True)
-    # the timed batches run without the scan's timing events (two stream markers per
-    # batch); the scan kernel's duration for the roofline comes from a separate timed pass
+    # the timed steps run without the scan's timing events (two stream markers per
+    # batch); the scan kernel's duration comes from a separate timed pass
     vts.set_timing(False)
     d.barrier()
     t0 = time.perf_counter()
-    if pipeline == 'stream':
-        sidx, _ = vts.match_stream((steps, Q, sbufs))
-    else:
-        for _ in range(steps):
+    results = []
+    for i in range(steps):
+        if pipeline == 'stream':
+            results.append(step(i))
+        else:
             match(staged=True)
     t1 = time.perf_counter()
     d.barrier()
     dt = d.max(t1 - t0)
     if pipeline == 'stream':
-        for b in range(steps):
-            h = srcs[b] >= 0
-            correct = correct and bool(np.all(sidx[b][h] == srcs[b][h]))
-        sbufs.close()
+        for (sidx, _), c in results:
+            for b in range(bpc):
+                s_ = srcs[c * bpc + b]
+                correct = correct and bool(np.all(sidx[b][s_ >= 0] == s_[s_ >= 0]))
+        bufs.close()
         match(staged=False)                  # re-stage one batch for the timed-scan pass
     vts.set_timing(True)
     kernel_ms = []
-    for _ in range(steps):
+    for _ in range(max(10, min(steps * bpc, 100))):
         match(staged=True)
         kernel_ms.append(vts.device_ms())
     # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
     d.barrier()
     p0 = time.perf_counter()
-    npcie = max(3, steps // 4)
+    npcie = max(3, min(steps * bpc // 4, 50))
     for _ in range(npcie):
         match(staged=False)
     p1 = time.perf_counter()
     d.barrier()
     dtp = d.max(p1 - p0)
     compares = float(total) * Q
-    scan_ms = float(np.mean(kernel_ms))
     res = {
-        'value': compares * steps / dt,
+        'value': compares * steps * bpc / dt,
         'ms_per_step': 1e3 * dt / steps,
+        'batches_per_step': bpc,
+        'timed_batches': steps * bpc,
+        'timed_region_s': dt,
         'pcie_inclusive_value': compares * npcie / dtp,
-        'scan_ms': scan_ms,
-        'kernel': SCAN_KERNELS[vts.scan_form()],
+        'scan_ms': float(np.mean(kernel_ms)),
+        'scan_ms_min': float(np.min(kernel_ms)),
+        'kernel': SCAN_KERNELS.get(vts.scan_form(), vts.scan_form()),
         'compares_per_launch': float(len(range(d.rank, total, n))) * Q,
+        'templates_per_launch': len(range(d.rank, total, n)),
         'reduce': reduce_kind,
         'pipeline': pipeline,
         'hits_correct': correct,
@@ -216,12 +248,58 @@ def bench_templates(args, d, total=None, steps=None, warmup=None):
     return res
 
 
-def pc_roofline(ncell, per_step_kernel_ms):
-    alg = 24.0 * ncell            # 3 stencil passes x (read + write) x 4 B
-    ach = alg / (per_step_kernel_ms * 1e-3) / 1e9
+def _traffic():
+    p = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    try:
+        return json.load(open(p))
+    except (OSError, ValueError):
+        return {}
+
+
+def scan_roofline(tv, tj, key):
+    """Roofline of one template-scan configuration: VALU-issue bound.  ``tj[key]``
+    holds the PMC VALU wave-instructions and HBM bytes per launch of the same
+    configuration (templates per launch, queries), from profiles/."""
+    rec = (tj.get('scans') or {}).get(key) or {}
+    same = (rec.get('templates_per_launch') == tv['templates_per_launch']
+            and rec.get('queries') is not None and rec.get('kernel', '').startswith(tv['kernel']))
+    scan_s = tv['scan_ms'] * 1e-3
+    roof = {'bound': 'valu', 'unit': 'G wave-instructions/s', 'peak': VALU_PEAK_GINSTS,
+            'achieved': None, 'frac': None, 'traffic': None,
+            'kernel_ms': tv['scan_ms'], 'kernel_time_source': 'HIP events around each scan launch'}
+    if same and rec.get('valu_insts_per_launch'):
+        vi = rec['valu_insts_per_launch']
+        roof['achieved'] = vi / scan_s / 1e9
+        roof['frac'] = roof['achieved'] / VALU_PEAK_GINSTS
+        roof['valu_insts_per_launch'] = vi
+        roof['traffic'] = rec.get('hbm_bytes_per_launch')
+        roof['source'] = 'profiles/' + rec.get('source', '')
+        if roof['traffic']:
+            roof['hbm_achieved_GBs'] = roof['traffic'] / scan_s / 1e9
+            roof['hbm_frac'] = roof['hbm_achieved_GBs'] / HBM_PEAK_GBS
+    # unique bytes a launch must move: the stored templates (bytes + planes + sums)
+    # once, the queries' planes once
+    uniq = tv['templates_per_launch'] * (2048 + 4096 + 64) + tv['compares_per_launch'] / max(
+        1, tv['templates_per_launch']) * (4 * 51 * 32 + 4)
+    roof['unique_bytes_per_launch'] = uniq
+    if roof['traffic']:
+        roof['traffic_over_unique'] = roof['traffic'] / uniq
+    roof['hbm_equivalent_GBs'] = BYTES_PER_COMPARE * tv['compares_per_launch'] / scan_s / 1e9
+    roof['note'] = ('frac = VALU issue rate / wave64 peak; hbm_equivalent_GBs = SURVEY 8(d) 2,048 '
+                    'B per compare / scan time, an equivalence (each template is reused by every '
+                    'query of the batch), not traffic')
+    return roof
+
+
+def pc_roofline(ncell, us_per_step, traffic=None):
+    """24 algorithmic B per cell per step over the measured wall
+    time per batched step (>= the kernels' time, so frac is a lower bound)."""
+    alg = 24.0 * ncell
+    ach = alg / (us_per_step * 1e-6) / 1e9
     return {'bound': 'hbm', 'achieved': ach, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-            'frac': ach / HBM_PEAK_GBS, 'traffic': None,
-            'note': '24 B/cell/step algorithmic over the two kernels\' summed HIP-event time'}
+            'frac': ach / HBM_PEAK_GBS, 'traffic': traffic,
+            'algorithmic_bytes_per_step': alg,
+            'note': '24 B/cell/step algorithmic (SURVEY 8(d)) / wall time per batched step'}
 
 
 def bench_posecell_stress(args, d):
@@ -249,9 +327,9 @@ def bench_posecell_stress(args, d):
     net.close()
     ncell = shape[0] * shape[1] * shape[2]
     return {'shape': list(shape), 'steps_per_s': n / dt, 'us_per_step': 1e6 * dt / n,
-            'kernel_us_per_step': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
+            'kernel_us_per_step_events': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
             'step_form': form, 'finite': finite,
-            'roofline': pc_roofline(ncell, (ex_ms + pi_ms) / nprof)}
+            'roofline': pc_roofline(ncell, 1e6 * dt / n)}
 
 
 def bench_posecells(args, d):
@@ -275,31 +353,48 @@ def bench_posecells(args, d):
     for v in od[base + 16:base + 16 + args.pc_calls]:
         net.update(v)
     c1 = time.perf_counter()
-    # kernel durations (HIP events around every launch) on a separate profiled run
+    # kernel durations (HIP events around every launch, which add gaps) on a separate run
     nprof = min(args.pc_steps, 500)
     net.set_profiling(True)
     net.run(od[:nprof])
     ex_ms, pi_ms = net.kernel_ms()
     net.set_profiling(False)
-    per_step_kernel_ms = (ex_ms + pi_ms) / nprof
     ncell = shape[0] * shape[1] * shape[2]
     finite = bool(np.isfinite(net.posecells).all())
     form = net.step_form()
     net.close()
-    roof = pc_roofline(ncell, per_step_kernel_ms)
-    roof['note'] += ('; the 576 KiB volume is L2-resident and the step is launch/latency-bound '
-                     'at this size (see pose_cell_stress for configs[3])')
+    roof = pc_roofline(ncell, 1e6 * dt / args.pc_steps)
+    roof['note'] += ('; the 576 KiB volume is L2-resident and the step is launch/latency-bound at '
+                     'this size (see pose_cell_stress for configs[3])')
     return {
         'shape': list(shape),
         'steps_per_s': args.pc_steps / dt,
         'update_calls_per_s': args.pc_calls / (c1 - c0),
         'us_per_step': 1e6 * dt / args.pc_steps,
-        'kernel_us_per_step': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
+        'kernel_us_per_step_events': {'excite': 1e3 * ex_ms / nprof, 'path': 1e3 * pi_ms / nprof},
         'replicas': d.world,
         'step_form': form,
         'finite': finite,
         'roofline': roof,
     }
+
+
+def host_info():
+    model = platform.processor() or ''
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = None
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        pass
+    return {'cpu_model': model, 'os_cpu_count': os.cpu_count(), 'affinity_cpus': aff,
+            'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
 
 
 def cpu_baseline(args):
@@ -313,6 +408,7 @@ def cpu_baseline(args):
     lib = synthetic.library(T, seed=1)
     qs, _ = synthetic.queries(lib, 4096, seed=2)
     budget = args.cpu_seconds
+    host = host_info()
     # C / OpenMP: template compares
     n = 0
     t0 = time.perf_counter()
@@ -322,8 +418,8 @@ def cpu_baseline(args):
     dt = time.perf_counter() - t0
     threads = C.threads()
     vt = {'value': T * n / dt, 'unit': 'compares/s', 'cores': threads, 'kind': 'port',
-          'sample': '%d queries x %d stored 64x32 u8 templates, oracle/c (C restatement of '
-                    'view_templates.py, OpenMP %d threads)' % (n, T, threads)}
+          'sample': '%d queries x %d stored 64x32 u8 templates in %.1f s, oracle/c (C restatement '
+                    'of view_templates.py, OpenMP %d threads)' % (n, T, dt, threads), **host}
     # NumPy, single thread
     n = 0
     t0 = time.perf_counter()
@@ -332,7 +428,7 @@ def cpu_baseline(args):
         n += 1
     dt = time.perf_counter() - t0
     vt_np = {'value': T * n / dt, 'unit': 'compares/s', 'cores': 1, 'kind': 'port',
-             'sample': '%d queries, oracle/view_templates.py (NumPy)' % n}
+             'sample': '%d queries in %.1f s, oracle/view_templates.py (NumPy)' % (n, dt)}
     shape = tuple(int(s) for s in args.pc_shape.split(','))
     od = synthetic.odometry(100000, seed=0)
     res = {}
@@ -347,12 +443,12 @@ def cpu_baseline(args):
         res[name] = (k, time.perf_counter() - t0)
     k, dt = res['c']
     pc = {'value': k / dt, 'unit': 'steps/s', 'cores': threads, 'kind': 'port',
-          'sample': '%d updates of a %s grid, oracle/c (C restatement of the three OpenCL '
-                    'kernels in float64, 343-tap direct correlation, OpenMP %d threads; host '
-                    'control in NumPy)' % (k, shape, threads)}
+          'sample': '%d updates of a %s grid in %.1f s, oracle/c (C restatement of the three '
+                    'OpenCL kernels in float64, 343-tap direct correlation, OpenMP %d threads; '
+                    'host control in NumPy)' % (k, shape, dt, threads), **host}
     k, dt = res['numpy']
     pc_np = {'value': k / dt, 'unit': 'steps/s', 'cores': 1, 'kind': 'port',
-             'sample': '%d updates, oracle/posecell.py (NumPy float64)' % k}
+             'sample': '%d updates in %.1f s, oracle/posecell.py (NumPy float64)' % (k, dt)}
     return vt, vt_np, pc, pc_np
 
 
@@ -366,13 +462,13 @@ def bench_replay(args, d):
     replay.RatslamReplay(device=d.dev).replay_events(events[:40])   # warm-up: kernels, allocations
     vts, reduce_kind = None, 'none'
     if d.world > 1 and args.same_device:
-        vts, reduce_kind = replay.sharded_templates(d, d.dev, gloo=True), 'gloo-host-min'
+        vts, reduce_kind = replay.sharded_templates(d, d.dev, host_reduce=True), 'host-tcp-min'
     elif d.world > 1:
         try:
             vts, reduce_kind = replay.sharded_templates(d, d.dev), 'rccl-allreduce-min-u64'
         except Exception as e:  # pragma: no cover - recorded, not hidden
-            print('rank %d: RCCL attach failed (%s); host gloo reduction' % (d.rank, e), file=sys.stderr)
-            vts, reduce_kind = replay.sharded_templates(d, d.dev, gloo=True), 'gloo-host-min'
+            print('rank %d: RCCL attach failed (%s); host reduction' % (d.rank, e), file=sys.stderr)
+            vts, reduce_kind = replay.sharded_templates(d, d.dev, host_reduce=True), 'host-tcp-min'
     r = replay.RatslamReplay(device=d.dev, vts=vts)
     d.barrier()
     t0 = time.perf_counter()
@@ -389,60 +485,39 @@ def bench_replay(args, d):
 
 def main():
     args = parse()
+    if args.gpus > 1 and not launch.under_launcher():
+        # our own N ranks, started before this process touches the GPU
+        sys.exit(launch.spawn(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
     d = Dist(args.gpus)
     # the GPU of this rank; --same-device puts every rank on GPU 0 (a test aid for
     # 1-GPU boxes: RCCL refuses two ranks on one GPU, so the host reducer is used)
     d.dev = 0 if args.same_device else d.local
-    tv = bench_templates(args, d)
+    tv = bench_templates(args, d, per_gpu=args.templates_per_gpu)
     lib100 = None
     if args.library_total > 0:
         lib100 = bench_templates(args, d, total=args.library_total, steps=args.library_steps,
-                                 warmup=1)
+                                 warmup=1, bps=2)
     pc = bench_posecells(args, d)
-    pcs = None if args.no_pc_stress else bench_posecell_stress(args, d)
+    pcs, st = None, None
+    if not args.no_pc_stress:
+        pcs = bench_posecell_stress(args, d)
+        if args.stress_templates > 0:
+            st = bench_templates(args, d, per_gpu=args.stress_templates, steps=4, warmup=1, bps=5)
     rp = None if args.no_replay else bench_replay(args, d)
     if d.rank != 0:
         d.close()
         return
-    roof = {
-        'bound': 'hbm',
-        'achieved': BYTES_PER_COMPARE * tv['compares_per_launch'] / (tv['scan_ms'] * 1e-3) / 1e9,
-        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-        'traffic': None,
-    }
-    roof['frac'] = roof['achieved'] / roof['peak']
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if (tj.get('templates_per_gpu') == args.templates_per_gpu and tj.get('queries') == args.queries
-                    and tj.get('kernel', '').startswith(tv['kernel'])):
-                roof['traffic'] = tj.get('hbm_bytes_per_launch')
-                roof['traffic_source'] = os.path.relpath(args.traffic_json, ROOT)
-                vi = tj.get('valu_insts_per_launch')
-                if vi:
-                    # the scan is VALU-bound: wave64 VALU issue peaks at one instruction per
-                    # 2 cycles per SIMD (1024 SIMDs, 2.4 GHz)
-                    ach = vi / (tv['scan_ms'] * 1e-3) / 1e9
-                    roof['valu'] = {'insts_per_launch': vi, 'achieved': ach,
-                                    'peak': VALU_PEAK_GINSTS, 'unit': 'G wave-instructions/s',
-                                    'frac': ach / VALU_PEAK_GINSTS}
-        except Exception:
-            pass
-    # measured HBM bytes of the pose-cell kernels (same PMC passes), per step form
-    tj_pc = {}
-    if os.path.exists(args.traffic_json):
-        try:
-            tj_pc = json.load(open(args.traffic_json)).get('pose_cell', {})
-        except Exception:
-            tj_pc = {}
+    tj = _traffic()
+    roof = scan_roofline(tv, tj, 'headline')
+    tj_pc = tj.get('pose_cell', {})
     for leg in (pc, pcs):
         if leg and leg['step_form'] in tj_pc:
-            leg['roofline']['traffic'] = tj_pc[leg['step_form']]['hbm_bytes_per_step']
-            leg['roofline']['traffic_kernels'] = tj_pc[leg['step_form']]['kernels']
-    roof['note'] = ('achieved = 2,048 algorithmic bytes per compare (SURVEY.md 8(d)) / scan time; '
-                    'above the HBM peak because each template is read from HBM once per batch and '
-                    'reused from registers by all queries (traffic = measured HBM bytes per launch); '
-                    'the kernel is bound by VALU issue, see valu')
+            rec = tj_pc[leg['step_form']]
+            if rec.get('shape') in (None, leg['shape']):
+                leg['roofline']['traffic'] = rec.get('hbm_bytes_per_step')
+                leg['roofline']['traffic_kernels'] = rec.get('kernels')
+                if rec.get('kernel_us_rocprof'):
+                    leg['kernel_us_per_step_rocprof'] = rec['kernel_us_rocprof']
     out = {
         'metric': METRIC,
         'value': tv['value'],
@@ -459,10 +534,14 @@ def main():
                 'U(0,0.6) m / U(-0.15,0.15) rad odometry)',
         'config': {
             'workload': 'configs[1]: 64x64x36 pose-cell grid + %d stored 64x32 u8 templates per '
-                        'GPU, %d-query batches resident in HBM' % (args.templates_per_gpu, args.queries),
+                        'GPU; a step matches %d batches of %d queries resident in HBM'
+                        % (args.templates_per_gpu, tv['batches_per_step'], args.queries),
             'templates_per_gpu': args.templates_per_gpu,
             'templates_total': tv['templates_total'],
-            'queries_per_step': args.queries,
+            'queries_per_batch': args.queries,
+            'batches_per_step': tv['batches_per_step'],
+            'timed_batches': tv['timed_batches'],
+            'timed_region_s': tv['timed_region_s'],
             'template_shape': [64, 32],
             'pose_cell_grid': pc['shape'],
             'parallelism': 'library sharded over %d GPU(s), %s; pose cells replicated'
@@ -475,19 +554,30 @@ def main():
                             lib100['templates_total'], d.world, args.queries),
             'scaling': 'strong', 'compares_per_s': lib100['value'],
             'ms_per_step': lib100['ms_per_step'], 'steps': args.library_steps,
+            'batches_per_step': lib100['batches_per_step'],
             'scan_ms_per_launch': lib100['scan_ms'], 'kernel': lib100['kernel'],
             'compares_per_launch_per_gpu': lib100['compares_per_launch'],
             'reduce': lib100['reduce'], 'pipeline': lib100['pipeline'],
             'known_answer_hits_correct': lib100['hits_correct'],
-            'pcie_inclusive_compares_per_s': lib100['pcie_inclusive_value']},
+            'pcie_inclusive_compares_per_s': lib100['pcie_inclusive_value'],
+            'roofline': scan_roofline(lib100, tj, 'library') if d.world == 1 else None},
         'pose_cell': pc,
         'pose_cell_stress': pcs,
         'replay': rp,
         'template_scan': {'kernel': tv['kernel'], 'kernel_ms_per_launch': tv['scan_ms'],
+                          'kernel_ms_per_launch_min': tv['scan_ms_min'],
                           'pipeline': tv['pipeline'],
                           'pcie_inclusive_compares_per_s': tv['pcie_inclusive_value'],
                           'known_answer_hits_correct': tv['hits_correct']},
     }
+    if pcs is not None and st is not None:
+        pcs['templates'] = {
+            'workload': 'configs[3]: %d stored 64x32 u8 templates per GPU, %d-query batches '
+                        'resident in HBM' % (args.stress_templates, args.queries),
+            'compares_per_s': st['value'], 'ms_per_step': st['ms_per_step'],
+            'batches_per_step': st['batches_per_step'], 'scan_ms_per_launch': st['scan_ms'],
+            'kernel': st['kernel'], 'known_answer_hits_correct': st['hits_correct'],
+            'roofline': scan_roofline(st, tj, 'stress')}
     if d.world == 1 and not args.no_cpu_baseline:
         vt_cpu, vt_np, pc_cpu, pc_np = cpu_baseline(args)
         out['cpu_baseline'] = vt_cpu

@@ -32,6 +32,9 @@
  *                   semantics incl. in-batch appends), or a frozen-library scan
  *   rs_vt_match_stream  many frozen-library batches, one host synchronisation
  *   rs_vt_read      ViewTemplate.template         view_templates.py:11
+ *   rs_vt_scores    ViewTemplate.match per pair   view_templates.py:16-28 (uint8, wrapping)
+ *   rs_sad_scores   ViewTemplate.match per pair   view_templates.py:16-28 (float32/float64)
+ *   rs_vt_set_threshold  the `min(match_val) > match_threshold` rule, view_templates.py:67
  *   rs_vt_set_subsample / rs_vt_match_frames
  *                   input[self.mask].reshape(...) view_templates.py:48-57,64 (on device)
  *   rs_comm_*, rs_vt_attach_comm  (new) RCCL sharding of the library over GPUs
@@ -232,9 +235,28 @@ int rs_vt_last_ms(rs_vt* h, double* ms);
  * match call (a ~5 us gap between the scan and the result export) */
 int rs_vt_set_timing(rs_vt* h, int enable);
 /* which scan kernel family the handle uses for its shape: "plane" (bit-plane
- * borrow count, W == 32, H in {32, 64}, max_offset 8), "carry", "sad", "rb2",
- * "rb3" (byte-SWAR forms, RS_VT_SCAN) or "generic"; NULL for a null handle */
+ * borrow count, W == 32, H in {32, 64}, max_offset 8), "carry" (byte-SWAR carry
+ * count, max_offset 8, H in {32, 64}; RS_VT_SCAN=carry forces it) or "generic";
+ * NULL for a null handle */
 const char* rs_vt_scan_form(const rs_vt* h);
+
+/* ViewTemplates.match's strict threshold (view_templates.py:67) as a double: a
+ * score makes a new template when (double)score > threshold -- numpy's own
+ * comparison of a uint64 score with a Python float (inf: never once the library
+ * is non-empty; negative: always; NaN: never).  rs_vt_create's integer threshold
+ * is the same rule for thresholds that are integers. */
+int rs_vt_set_threshold(rs_vt* h, double threshold);
+
+/* ViewTemplate.match on float arrays (view_templates.py:16-28 with float32 or
+ * float64 data: no uint8 wrap, a true sum |T - Q| per row offset in the arrays'
+ * precision, numpy's pairwise summation order, first strict minimum over the
+ * 2*max_offset-1 offsets from +inf).  templates[nt*H*W], queries[nq*H*W] and
+ * scores[nq*nt] (scores[q*nt + t]) are host arrays of dtype RS_DT_F32 / F64;
+ * the scores are computed on `device`. */
+#define RS_DT_F32 0
+#define RS_DT_F64 1
+int rs_sad_scores(int device, int dtype, int H, int W, int max_offset, int64_t nt,
+                  const void* templates, int nq, const void* queries, void* scores);
 
 /* Multi-GPU: one process per GPU, library sharded round-robin (template g lives
  * on rank g % nranks at slot g / nranks); per query the local first-argmin keys

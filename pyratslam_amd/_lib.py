@@ -27,6 +27,8 @@ RS_PREC_F64 = 1
 RS_VT_FROZEN = 0
 RS_VT_SEQUENTIAL = 1
 RS_UNIQUE_ID_BYTES = 128
+RS_DT_F32 = 0
+RS_DT_F64 = 1
 FILTER_LEN = 7
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -101,6 +103,9 @@ SIGNATURES = {
     'rs_vt_last_ms': (ctypes.c_int, [_vp, _f64p]),
     'rs_vt_set_timing': (ctypes.c_int, [_vp, ctypes.c_int]),
     'rs_vt_scan_form': (ctypes.c_char_p, [_vp]),
+    'rs_vt_set_threshold': (ctypes.c_int, [_vp, ctypes.c_double]),
+    'rs_sad_scores': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int64, _vp, ctypes.c_int, _vp, _vp]),
     'rs_comm_unique_id': (ctypes.c_int, [_u8p]),
     'rs_vt_attach_comm': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _u8p]),
     'rs_vt_set_shard': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
@@ -189,6 +194,13 @@ class DeviceBuffer:
         check(self._lib.rs_dev_copy(self.ptr, ctypes.c_void_p(a.ctypes.data), a.nbytes))
         return self
 
+    def offset(self, byte_offset):
+        """A view of the buffer from ``byte_offset`` on (``ptr`` / ``nbytes``), kept
+        valid by a reference to this buffer."""
+        if not 0 <= byte_offset <= self.nbytes:
+            raise ValueError('offset %d outside the %d-byte buffer' % (byte_offset, self.nbytes))
+        return DeviceView(self, int(byte_offset))
+
     def close(self):
         if getattr(self, 'ptr', None) is not None and self.ptr.value:
             self._lib.rs_dev_free(self.ptr)
@@ -199,3 +211,12 @@ class DeviceBuffer:
             self.close()
         except Exception:
             pass
+
+
+class DeviceView:
+    """``DeviceBuffer.offset``: a sub-range of a device buffer."""
+
+    def __init__(self, base, byte_offset):
+        self._base = base
+        self.ptr = ctypes.c_void_p(base.ptr.value + byte_offset)
+        self.nbytes = base.nbytes - byte_offset

@@ -142,202 +142,6 @@ __device__ inline void emit_score(const ScanOut& out, int64_t slot, int64_t coun
     }
 }
 
-// --- throughput form: one lane per template, 64 templates x NQ queries per wave.
-// Query forms are wave-uniform (scalar loads); each template dword is hoisted
-// once into (a & 0x7f7f7f7f, a & 0x80808080) and reused by the 2M-1 offsets.
-template <int H, int NQ, bool MATRIX>
-__global__ __launch_bounds__(64) void vt_scan_lane_kernel(const uint4* __restrict__ lib, int ntb,
-                                                          int64_t count, int WD,
-                                                          const uint2* __restrict__ qf, int nq,
-                                                          ScanOut out, int rank, int nranks) {
-    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
-    // XCD-aware mapping (speed only): blocks b and b+8 are dealt to the same XCD, so
-    // XCD x takes query groups qg = x (mod 8) against the whole library -- its L2
-    // holds the library plus 1/8 of the query forms.
-    const int j = blockIdx.x >> 3;
-    const int tb = j % ntb;
-    const int qg = (j / ntb) * 8 + (blockIdx.x & 7);
-    if (qg * NQ >= nq) return;
-    const int qbase = qg * NQ;
-    const int lane = threadIdx.x;
-    uint32_t acc[NQ][NO];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n)
-#pragma unroll
-        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
-
-    for (int c = 0; c < WD; ++c) {
-        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + lane;
-        uint32_t aL[4 * HQ], aH[4 * HQ];
-#pragma unroll
-        for (int q = 0; q < HQ; ++q) {
-            const uint4 v = col[(size_t)q * 64];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
-                aH[4 * q + k] = w[k] & 0x80808080u;
-            }
-        }
-#pragma unroll
-        for (int r = M; r < H - M; ++r) {
-#pragma unroll
-            for (int n = 0; n < NQ; ++n) {
-                const int qi = min(qbase + n, nq - 1);
-                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
-#pragma unroll
-                for (int o = 0; o < NO; ++o) {
-                    const int s = r + o - (M - 1);
-                    acc[n][o] = wrapped_pair(aL[s], aH[s], f, acc[n][o]);
-                }
-            }
-        }
-    }
-    const int64_t slot = (int64_t)tb * 64 + lane;
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-        uint32_t sc = acc[n][0];
-#pragma unroll
-        for (int o = 1; o < NO; ++o) sc = min(sc, acc[n][o]);
-        emit_score<MATRIX>(out, slot, count, qbase + n, nq, sc, rank, nranks, lane == 0);
-    }
-}
-
-// --- row-blocked throughput form: the query rows [M, H-M) of a column are split
-// into RB blocks; a block hoists only the template rows its 2M-1 offsets touch
-// (RS + 2M - 2 rows instead of H), which keeps the kernel near 128 VGPRs (4 waves
-// per SIMD) at the cost of re-reading the overlapping quads (L1 hits).
-template <int H, int NQ, int RB, int B>
-__device__ inline void scan_block(const uint4* __restrict__ col, const uint2* __restrict__ qf,
-                                  int WD, int c, int qbase, int nq, uint32_t (&acc)[NQ][2 * FAST_M - 1]) {
-    constexpr int M = FAST_M, NO = 2 * M - 1, R0 = M, R1 = H - M;
-    constexpr int RS = (R1 - R0 + RB - 1) / RB;
-    constexpr int r_lo = R0 + B * RS;
-    constexpr int r_hi = (r_lo + RS < R1) ? r_lo + RS : R1;
-    constexpr int s_lo = r_lo - (M - 1), s_hi = r_hi - 1 + (M - 1);
-    constexpr int q_lo = s_lo / 4, q_hi = s_hi / 4, NQD = q_hi - q_lo + 1;
-    uint32_t aL[4 * NQD], aH[4 * NQD];
-#pragma unroll
-    for (int q = 0; q < NQD; ++q) {
-        const uint4 v = col[(size_t)(q_lo + q) * 64];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
-            aH[4 * q + k] = w[k] & 0x80808080u;
-        }
-    }
-#pragma unroll
-    for (int r = r_lo; r < r_hi; ++r) {
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-            const int qi = min(qbase + n, nq - 1);
-            const uint2 f = qf[((size_t)qi * WD + c) * H + r];
-#pragma unroll
-            for (int o = 0; o < NO; ++o) {
-                const int sidx = r + o - (M - 1) - 4 * q_lo;
-                acc[n][o] = wrapped_pair(aL[sidx], aH[sidx], f, acc[n][o]);
-            }
-        }
-    }
-    if constexpr (B + 1 < RB) scan_block<H, NQ, RB, B + 1>(col, qf, WD, c, qbase, nq, acc);
-}
-
-template <int H, int NQ, int RB, bool MATRIX>
-__global__ __launch_bounds__(64) void vt_scan_rb_kernel(const uint4* __restrict__ lib, int ntb,
-                                                        int64_t count, int WD,
-                                                        const uint2* __restrict__ qf, int nq,
-                                                        ScanOut out, int rank, int nranks) {
-    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
-    const int j = blockIdx.x >> 3;
-    const int tb = j % ntb;
-    const int qg = (j / ntb) * 8 + (blockIdx.x & 7);
-    if (qg * NQ >= nq) return;
-    const int qbase = qg * NQ;
-    const int lane = threadIdx.x;
-    uint32_t acc[NQ][NO];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n)
-#pragma unroll
-        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
-    for (int c = 0; c < WD; ++c)
-        scan_block<H, NQ, RB, 0>(lib + ((size_t)(tb * WD + c) * HQ) * 64 + lane, qf, WD, c, qbase,
-                                 nq, acc);
-    const int64_t slot = (int64_t)tb * 64 + lane;
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-        uint32_t sc = acc[n][0];
-#pragma unroll
-        for (int o = 1; o < NO; ++o) sc = min(sc, acc[n][o]);
-        emit_score<MATRIX>(out, slot, count, qbase + n, nq, sc, rank, nranks, lane == 0);
-    }
-}
-
-// --- latency form: 8 lanes per template (one dword column each), 8 templates
-// per wave; the per-offset sums are combined across the 8 column lanes.
-template <int H, int NQ>
-__global__ __launch_bounds__(64) void vt_scan_col_kernel(const uint4* __restrict__ lib,
-                                                         int64_t count, int WD,
-                                                         const uint2* __restrict__ qf, int nq,
-                                                         ScanOut out, int rank, int nranks) {
-    constexpr int M = FAST_M, HQ = (H + 3) / 4, NO = 2 * M - 1;
-    const int lane = threadIdx.x;
-    const int t8 = lane >> 3, cl = lane & 7;
-    const int64_t slot = (int64_t)blockIdx.x * 8 + t8;
-    const int64_t tb = slot >> 6, tl = slot & 63;
-    const int qbase = blockIdx.y * NQ;
-    uint32_t acc[NQ][NO];
-#pragma unroll
-    for (int n = 0; n < NQ; ++n)
-#pragma unroll
-        for (int o = 0; o < NO; ++o) acc[n][o] = 0u;
-
-    for (int c = cl; c < WD; c += 8) {
-        const uint4* col = lib + ((size_t)(tb * WD + c) * HQ) * 64 + tl;
-        uint32_t aL[4 * HQ], aH[4 * HQ];
-#pragma unroll
-        for (int q = 0; q < HQ; ++q) {
-            const uint4 v = col[(size_t)q * 64];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                aL[4 * q + k] = w[k] & 0x7F7F7F7Fu;
-                aH[4 * q + k] = w[k] & 0x80808080u;
-            }
-        }
-#pragma unroll
-        for (int r = M; r < H - M; ++r) {
-#pragma unroll
-            for (int n = 0; n < NQ; ++n) {
-                const int qi = min(qbase + n, nq - 1);
-                const uint2 f = qf[((size_t)qi * WD + c) * H + r];
-#pragma unroll
-                for (int o = 0; o < NO; ++o) {
-                    const int s = r + o - (M - 1);
-                    acc[n][o] = wrapped_pair(aL[s], aH[s], f, acc[n][o]);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < NQ; ++n) {
-        uint32_t sc = 0xFFFFFFFFu;
-#pragma unroll
-        for (int o = 0; o < NO; ++o) {
-            uint32_t v = acc[n][o];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            sc = min(sc, v);
-        }
-        const unsigned long long g = (unsigned long long)slot * nranks + rank;
-        unsigned long long key =
-            (slot < count && cl == 0) ? (((unsigned long long)sc << 32) | g) : NO_KEY;
-        key = wave_min_u64(key);
-        if (lane == 0 && qbase + n < nq) atomicMin(out.best + qbase + n, key);
-    }
-}
-
 // --- carry-count forms.  v_sad_u8 issues at half rate on gfx950 (measured,
 // tools/ubench_valu.hip), so the byte sum is taken apart exactly:
 //   sum_b (a_b + c_b) mod 256 = bytesum(a) + bytesum(c) - 256 * #carries,
@@ -875,6 +679,88 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     VT_STAMP(1);
 }
 
+// ===========================================================================
+// Float path of ViewTemplate.match (view_templates.py:16-28 with float arrays):
+// no wrap, a true sum of |T - Q| per row offset in the arrays' own precision,
+// summed in numpy's order -- np.sum of the contiguous (H-2M) x W difference is
+// numpy's pairwise summation over the flattened n elements (blocks of <= 128
+// with 8 strided accumulators, halves split at a multiple of 8), so the host
+// lowers that recursion for this n into a postfix program of leaf sums and adds
+// (int2 (start, len) = push the leaf's sum; (-1, 0) = pop two, push their sum)
+// that every thread evaluates: the same additions in the same order, bit-exact.
+// Then the first strict minimum over the offsets from +inf, as the reference's
+// `if diff < mindiff` loop (an all-NaN pair stays +inf).
+// ===========================================================================
+template <typename T>
+__device__ inline T sad_at(const T* __restrict__ a, const T* __restrict__ b, int W, int M, int o,
+                           int i) {
+    const int r = i / W, c = i - r * W;
+    const T d = a[(size_t)(M + o + r) * W + c] - b[(size_t)(M + r) * W + c];
+    if constexpr (sizeof(T) == 4) return fabsf(d);   // numpy's absolute is fabs
+    else return fabs(d);
+}
+
+template <typename T>
+__device__ T sad_leaf(const T* a, const T* b, int W, int M, int o, int s, int n) {
+    if (n < 8) {
+        T res = T(0);
+        for (int i = 0; i < n; ++i) res += sad_at(a, b, W, M, o, s + i);
+        return res;
+    }
+    T r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = sad_at(a, b, W, M, o, s + j);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += sad_at(a, b, W, M, o, s + i + j);
+    T res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += sad_at(a, b, W, M, o, s + i);
+    return res;
+}
+
+constexpr int SAD_STACK = 40;   // pairwise depth: log2(n / 128) + 2 <= 40 for any n < 2^31
+
+// 4 (template, query) pairs per 64-thread block, 16 threads per pair (one per offset)
+template <typename T>
+__global__ __launch_bounds__(64) void vt_sad_float_kernel(const T* __restrict__ tpl, int64_t nt,
+                                                          const T* __restrict__ qry, int nq, int H,
+                                                          int W, int M,
+                                                          const int2* __restrict__ prog, int nprog,
+                                                          T* __restrict__ out) {
+    __shared__ T s_d[4][16];
+    const int sub = threadIdx.x >> 4, oi = threadIdx.x & 15, NO = 2 * M - 1;
+    const int64_t pair = (int64_t)blockIdx.x * 4 + sub;
+    const bool live = pair < nt * (int64_t)nq;
+    const int64_t t = live ? pair % nt : 0, qi = live ? pair / nt : 0;
+    T d = T(INFINITY);
+    if (live && oi < NO) {
+        const T* a = tpl + (size_t)t * H * W;
+        const T* b = qry + (size_t)qi * H * W;
+        const int o = oi - (M - 1);
+        T st[SAD_STACK];
+        int sp = 0;
+        for (int k = 0; k < nprog; ++k) {
+            const int2 op = prog[k];
+            if (op.x >= 0) {
+                st[sp++] = sad_leaf(a, b, W, M, o, op.x, op.y);
+            } else {
+                const T rhs = st[--sp];
+                st[sp - 1] = st[sp - 1] + rhs;
+            }
+        }
+        d = st[0];
+    }
+    if (oi < 16) s_d[sub][oi] = d;
+    __syncthreads();
+    if (live && oi == 0) {
+        T best = T(INFINITY);
+        for (int k = 0; k < NO; ++k)
+            if (s_d[sub][k] < best) best = s_d[sub][k];
+        out[(size_t)qi * nt + t] = best;
+    }
+}
+
 // The batch's first-argmin keys -> the pinned host buffer (system-scope stores),
 // and the device keys reset to UINT64_MAX for the next scan: one queued launch in
 // place of a device-to-host blit copy and a memset before the next scan.
@@ -893,7 +779,10 @@ __global__ __launch_bounds__(256) void vt_keys_export(unsigned long long* __rest
 // ===========================================================================
 struct rs_vt {
     int H = 0, W = 0, M = 0, WD = 0, HQ = 0;
-    uint64_t thr = 0;
+    // ViewTemplates.match's threshold (view_templates.py:67): a score (< 2^32, exact in
+    // a double) makes a new template when score > thr, compared in float64 exactly as
+    // numpy compares a uint64 with a Python float (NaN: never; negative: always)
+    double thr = 0.0;
     int device = 0;
     int rank = 0, nranks = 1;
     ncclComm_t comm = nullptr;
@@ -937,8 +826,6 @@ struct rs_vt {
     bool timedScan = false;  // the last scan recorded ev0/ev1
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
-    bool carry = true;  // carry-count scan or v_sad_u8 scan (RS_VT_SCAN=sad)
-    int scan_rb = 0;    // row-blocked v_sad_u8 scan with this many row blocks (RS_VT_SCAN=rb2|rb3)
     // bit-plane scan (default when W == 32, H in {32, 64}, max_offset 8; RS_VT_SCAN=plane):
     // planes + TS of the library and candidate slots, query planes + raw sums
     bool planar = false;
@@ -1198,7 +1085,7 @@ int plane_split(int ntb, int nbatch, int slots) {
 // Launch a scan of queries [0, nq) (forms in dQf) against `count` slots of lib.
 template <bool MATRIX>
 int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
-                    int nranks) {
+                    int nranks, int64_t tb0) {
     const int ntb = (int)((count + 63) / 64);
     const int nqc = plane_split(ntb, (nq + PL_NB - 1) / PL_NB, h->planeSlots);
     if (8 * ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
@@ -1212,8 +1099,9 @@ int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int
     }
     RS_CHECK((int64_t)ntb * nqc < (1ll << 31), RS_ERR_ARG, "scan grid too large");
     const dim3 grid((unsigned)(ntb * nqc));
-    const uint4* planes = reinterpret_cast<const uint4*>(cand ? h->dCandP : h->dLibP);
-    const uint32_t* ts = cand ? h->dCandTs : h->dLibTs;
+    const uint4* planes = reinterpret_cast<const uint4*>(
+        reinterpret_cast<const uint8_t*>(cand ? h->dCandP : h->dLibP) + (size_t)tb0 * pblock_bytes(h));
+    const uint32_t* ts = (cand ? h->dCandTs : h->dLibTs) + (size_t)tb0 * (TS_BLOCK_BYTES / 4);
     if (h->H == 64)
         hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PL_CG * PL_SPLIT), 0, h->stream,
                            planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, h->dCtr, out, rank,
@@ -1226,62 +1114,38 @@ int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int
     return RS_OK;
 }
 
+// Launch a scan of queries [0, nq) against `count` slots of the library (or of
+// the candidate buffer), starting at 64-slot block tb0 of it.
 template <bool MATRIX>
 int vt_launch_scan(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
-                   int nranks) {
+                   int nranks, int64_t tb0 = 0) {
     if (count <= 0 || nq <= 0) return RS_OK;
-    if (h->planar) return vt_launch_plane<MATRIX>(h, cand, count, nq, out, rank, nranks);
-    const uint4* lib = cand ? h->dCand : h->dLib;
+    if (h->planar) return vt_launch_plane<MATRIX>(h, cand, count, nq, out, rank, nranks, tb0);
+    const uint4* lib = (cand ? h->dCand : h->dLib) + (size_t)tb0 * h->WD * h->HQ * 64;
     const int ntb = (int)((count + 63) / 64);
     const bool fast = h->M == FAST_M && (h->H == 64 || h->H == 32);
     RS_CHECK((int64_t)ntb * nq < (1ll << 31), RS_ERR_ARG, "scan grid too large (%d x %d)", ntb, nq);
     if (fast && !MATRIX && (int64_t)ntb * nq < 2048 && h->WD <= 8) {
         // few waves of work: spread each template over 8 column lanes
-        const int nb8 = (int)((count + 7) / 8);
-        const dim3 grid(nb8, nq);
-        if (h->carry) {
-            if (h->H == 64)
-                hipLaunchKernelGGL((vt_scan_carry_col_kernel<64, 1>), grid, dim3(64), 0, h->stream,
-                                   lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
-            else
-                hipLaunchKernelGGL((vt_scan_carry_col_kernel<32, 1>), grid, dim3(64), 0, h->stream,
-                                   lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
-        } else if (h->H == 64) {
-            hipLaunchKernelGGL((vt_scan_col_kernel<64, 1>), grid, dim3(64), 0, h->stream, lib,
-                               count, h->WD, h->dQf, nq, out, rank, nranks);
-        } else {
-            hipLaunchKernelGGL((vt_scan_col_kernel<32, 1>), grid, dim3(64), 0, h->stream, lib,
-                               count, h->WD, h->dQf, nq, out, rank, nranks);
-        }
+        const dim3 grid((unsigned)((count + 7) / 8), nq);
+        if (h->H == 64)
+            hipLaunchKernelGGL((vt_scan_carry_col_kernel<64, 1>), grid, dim3(64), 0, h->stream,
+                               lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
+        else
+            hipLaunchKernelGGL((vt_scan_carry_col_kernel<32, 1>), grid, dim3(64), 0, h->stream,
+                               lib, count, h->WD, h->dQf, h->dQsum, nq, out, rank, nranks);
     } else if (fast) {
         constexpr int NQ = 2;
         const int nqg = (nq + NQ - 1) / NQ;
         const dim3 grid((unsigned)(ntb * ((nqg + 7) / 8) * 8));
-        if (h->scan_rb == 2 && h->H == 64) {
-            hipLaunchKernelGGL((vt_scan_rb_kernel<64, NQ, 2, MATRIX>), grid, dim3(64), 0,
-                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        } else if (h->scan_rb == 3 && h->H == 64) {
-            hipLaunchKernelGGL((vt_scan_rb_kernel<64, NQ, 3, MATRIX>), grid, dim3(64), 0,
-                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        } else if (h->scan_rb == 2 && h->H == 32) {
-            hipLaunchKernelGGL((vt_scan_rb_kernel<32, NQ, 2, MATRIX>), grid, dim3(64), 0,
-                               h->stream, lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        } else if (h->carry) {
-            if (h->H == 64)
-                hipLaunchKernelGGL((vt_scan_carry_kernel<64, NQ, MATRIX>), grid, dim3(64), 0,
-                                   h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
-                                   rank, nranks);
-            else
-                hipLaunchKernelGGL((vt_scan_carry_kernel<32, NQ, MATRIX>), grid, dim3(64), 0,
-                                   h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
-                                   rank, nranks);
-        } else if (h->H == 64) {
-            hipLaunchKernelGGL((vt_scan_lane_kernel<64, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
-                               lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        } else {
-            hipLaunchKernelGGL((vt_scan_lane_kernel<32, NQ, MATRIX>), grid, dim3(64), 0, h->stream,
-                               lib, ntb, count, h->WD, h->dQf, nq, out, rank, nranks);
-        }
+        if (h->H == 64)
+            hipLaunchKernelGGL((vt_scan_carry_kernel<64, NQ, MATRIX>), grid, dim3(64), 0,
+                               h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
+                               rank, nranks);
+        else
+            hipLaunchKernelGGL((vt_scan_carry_kernel<32, NQ, MATRIX>), grid, dim3(64), 0,
+                               h->stream, lib, ntb, count, h->WD, h->dQf, h->dQsum, nq, out,
+                               rank, nranks);
     } else {
         hipLaunchKernelGGL((vt_scan_generic_kernel<MATRIX>), dim3((unsigned)(ntb * nq)), dim3(64),
                            0, h->stream, lib, ntb, count, h->H, h->M, h->WD, h->dQf, nq, out, rank,
@@ -1366,7 +1230,7 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
     // a template against every query once (replicated on all ranks).
     std::vector<int> cand;
     for (int i = 0; i < nq; ++i)
-        if (key[i] == NO_KEY || (key[i] >> 32) > h->thr) cand.push_back(i);
+        if (key[i] == NO_KEY || (double)(key[i] >> 32) > h->thr) cand.push_back(i);
     std::vector<int> cpos(nq, -1);
     int64_t ldm = 0;
     if (!cand.empty() && cand.front() < nq - 1) {
@@ -1397,7 +1261,7 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
                 (unsigned long long)news[a].second;
             k = kj < k ? kj : k;
         }
-        if (k == NO_KEY || (k >> 32) > h->thr) {
+        if (k == NO_KEY || (double)(k >> 32) > h->thr) {
             const int64_t g = h->count + (int64_t)news.size();
             news.emplace_back(i, g);
             if (is_new) is_new[i] = 1;
@@ -1567,16 +1431,19 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
     RS_CHECK(device >= 0 && device < ndev, RS_ERR_ARG, "device %d not in [0, %d)", device, ndev);
     RS_HIP(hipSetDevice(device));
     rs_vt* h = new rs_vt();
-    h->H = H; h->W = W; h->M = max_offset; h->thr = thr; h->device = device;
+    h->H = H; h->W = W; h->M = max_offset; h->thr = (double)thr; h->device = device;
     h->WD = (W + 3) / 4;
     h->HQ = (H + 3) / 4;
     h->planar = W == 8 * PL_CG && (H == 64 || H == 32) && max_offset == FAST_M;
     if (const char* e = std::getenv("RS_VT_SCAN")) {
-        // A/B switches for the byte-SWAR scans; "plane" (or unset) keeps the default
-        if (std::strcmp(e, "plane") != 0) h->planar = false;
-        h->carry = std::strcmp(e, "sad") != 0;
-        if (std::strcmp(e, "rb2") == 0) h->scan_rb = 2;
-        if (std::strcmp(e, "rb3") == 0) h->scan_rb = 3;
+        // A/B switch: "carry" forces the byte-SWAR carry-count scan; "plane" (or
+        // unset) keeps the default
+        if (std::strcmp(e, "carry") == 0) h->planar = false;
+        else if (std::strcmp(e, "plane") != 0 && e[0] != 0) {
+            rs::set_error("RS_VT_SCAN='%s': expected plane or carry", e);
+            delete h;
+            return RS_ERR_ARG;
+        }
     }
     if (h->planar) {
         // resident blocks per CU: the occupancy API, capped by the kernel's own VGPR and
@@ -1802,19 +1669,28 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
     RS_CHECK(queries && scores, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(vt_stage_queries(h, nq, queries));
-    h->stagedQ = nq;
-    const int64_t ld = (int64_t)rs::round_up((size_t)h->count, 64);
+    h->stagedQ = 0;  // the staging buffer no longer holds the last match batch
+    // only the 64-slot blocks that hold [t0, t0 + nt) are scanned
+    const int64_t tb0 = t0 / 64, lo = t0 - tb0 * 64, span = lo + nt;
+    const int64_t ld = (int64_t)rs::round_up((size_t)span, 64);
     RS_TRY(vt_grow_matrix(h, (size_t)ld * nq));
     ScanOut mo{nullptr, h->dMat, ld};
     RS_HIP(hipEventRecord(h->ev0, h->stream));
-    RS_TRY(vt_launch_scan<true>(h, false, h->count, nq, mo, 0, 1));
+    RS_TRY(vt_launch_scan<true>(h, false, span, nq, mo, 0, 1, tb0));
     RS_HIP(hipEventRecord(h->ev1, h->stream));
-    RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ld * nq, hipMemcpyDeviceToHost,
-                          h->stream));
+    RS_HIP(hipMemcpy2DAsync(h->hMat, sizeof(uint32_t) * nt, h->dMat + lo, sizeof(uint32_t) * ld,
+                            sizeof(uint32_t) * nt, nq, hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
-    for (int q = 0; q < nq; ++q)
-        for (int64_t t = 0; t < nt; ++t) scores[(size_t)q * nt + t] = h->hMat[(size_t)q * ld + t0 + t];
+    h->timedScan = true;
+    for (size_t i = 0; i < (size_t)nq * nt; ++i) scores[i] = h->hMat[i];
+    return RS_OK;
+}
+
+int rs_vt_set_threshold(rs_vt* h, double threshold) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
+    h->thr = threshold;
     return RS_OK;
 }
 
@@ -1822,9 +1698,7 @@ const char* rs_vt_scan_form(const rs_vt* h) {
     if (!h) return nullptr;
     if (h->planar) return "plane";
     if (h->M != FAST_M || (h->H != 64 && h->H != 32)) return "generic";
-    if (h->scan_rb == 2 && (h->H == 64 || h->H == 32)) return "rb2";
-    if (h->scan_rb == 3 && h->H == 64) return "rb3";
-    return h->carry ? "carry" : "sad";
+    return "carry";
 }
 
 int rs_vt_last_ms(rs_vt* h, double* ms) {
@@ -1869,6 +1743,74 @@ int rs_vt_attach_comm(rs_vt* h, int rank, int nranks, const uint8_t id[RS_UNIQUE
     h->rank = rank;
     h->nranks = nranks;
     return RS_OK;
+}
+
+// host side of the float path: numpy's pairwise program for n elements
+static void sad_program(int start, int n, std::vector<int2>& prog) {
+    if (n <= 128) {
+        prog.push_back(make_int2(start, n));
+        return;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    sad_program(start, n2, prog);
+    sad_program(start + n2, n - n2, prog);
+    prog.push_back(make_int2(-1, 0));
+}
+
+int rs_sad_scores(int device, int dtype, int H, int W, int max_offset, int64_t nt,
+                  const void* templates, int nq, const void* queries, void* scores) {
+    rs::clear_error();
+    RS_CHECK(dtype == RS_DT_F32 || dtype == RS_DT_F64, RS_ERR_TYPE, "dtype %d is not F32/F64", dtype);
+    RS_CHECK(H > 0 && W > 0 && max_offset >= 1 && max_offset <= 16 && H > 2 * max_offset,
+             RS_ERR_ARG, "bad shape (%d, %d) for max_offset %d", H, W, max_offset);
+    RS_CHECK((int64_t)H * W < (1ll << 31), RS_ERR_ARG, "template too large");
+    RS_CHECK(nt >= 0 && nq >= 0, RS_ERR_ARG, "negative count");
+    if (nt == 0 || nq == 0) return RS_OK;
+    RS_CHECK(templates && queries && scores, RS_ERR_ARG, "null argument");
+    int ndev = 0;
+    RS_HIP(hipGetDeviceCount(&ndev));
+    RS_CHECK(device >= 0 && device < ndev, RS_ERR_ARG, "device %d not in [0, %d)", device, ndev);
+    RS_HIP(hipSetDevice(device));
+    std::vector<int2> prog;
+    sad_program(0, (H - 2 * max_offset) * W, prog);
+    const size_t es = dtype == RS_DT_F32 ? 4 : 8;
+    const size_t tb = (size_t)nt * H * W * es, qb = (size_t)nq * H * W * es, ob = (size_t)nt * nq * es;
+    void *dT = nullptr, *dQ = nullptr, *dO = nullptr, *dP = nullptr;
+    hipStream_t st = nullptr;
+    int rc = RS_OK;
+    auto run = [&]() -> int {
+        RS_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        RS_HIP(hipMalloc(&dT, tb));
+        RS_HIP(hipMalloc(&dQ, qb));
+        RS_HIP(hipMalloc(&dO, ob));
+        RS_HIP(hipMalloc(&dP, sizeof(int2) * prog.size()));
+        RS_HIP(hipMemcpyAsync(dT, templates, tb, hipMemcpyHostToDevice, st));
+        RS_HIP(hipMemcpyAsync(dQ, queries, qb, hipMemcpyHostToDevice, st));
+        RS_HIP(hipMemcpyAsync(dP, prog.data(), sizeof(int2) * prog.size(), hipMemcpyHostToDevice, st));
+        const int64_t pairs = nt * (int64_t)nq;
+        RS_CHECK((pairs + 3) / 4 < (1ll << 31), RS_ERR_ARG, "too many pairs");
+        const dim3 grid((unsigned)((pairs + 3) / 4));
+        if (dtype == RS_DT_F32)
+            hipLaunchKernelGGL(vt_sad_float_kernel<float>, grid, dim3(64), 0, st,
+                               static_cast<const float*>(dT), nt, static_cast<const float*>(dQ), nq,
+                               H, W, max_offset, static_cast<const int2*>(dP), (int)prog.size(),
+                               static_cast<float*>(dO));
+        else
+            hipLaunchKernelGGL(vt_sad_float_kernel<double>, grid, dim3(64), 0, st,
+                               static_cast<const double*>(dT), nt, static_cast<const double*>(dQ),
+                               nq, H, W, max_offset, static_cast<const int2*>(dP), (int)prog.size(),
+                               static_cast<double*>(dO));
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemcpyAsync(scores, dO, ob, hipMemcpyDeviceToHost, st));
+        RS_HIP(hipStreamSynchronize(st));
+        return RS_OK;
+    };
+    rc = run();
+    for (void* p : {dT, dQ, dO, dP})
+        if (p) (void)hipFree(p);
+    if (st) (void)hipStreamDestroy(st);
+    return rc;
 }
 
 }  // extern "C"

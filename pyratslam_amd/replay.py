@@ -159,13 +159,14 @@ class RatslamReplay:
                 'templates': len(self.vts.templates)}
 
 
-def sharded_templates(d, device, gloo=False, x_range=X_RANGE, y_range=Y_RANGE, x_step=X_STEP,
+def sharded_templates(d, device, host_reduce=False, x_range=X_RANGE, y_range=Y_RANGE, x_step=X_STEP,
                       y_step=Y_STEP, im_size=IM_SIZE, match_threshold=MATCH_THRESHOLD):
     """The view-template library sharded over the ranks of ``d`` (a dist.Dist):
-    template g on rank g % N, one RCCL allreduce(min) per match (or the gloo
-    host reducer with ``gloo``, for several ranks on one GPU)."""
+    template g on rank g % N, one RCCL allreduce(min) per match (or the host
+    reducer of the control plane with ``host_reduce``, for several ranks on one
+    GPU)."""
     from .view_templates import ShardedViewTemplates
-    if gloo:
+    if host_reduce:
         return ShardedViewTemplates(x_range, y_range, x_step, y_step, im_size[0], im_size[1],
                                     match_threshold, d.rank, d.world, reducer=d.min_keys, device=device)
     uid = d.bcast_bytes(ShardedViewTemplates.unique_id() if d.rank == 0 else None)
@@ -184,15 +185,19 @@ def main(argv=None):
     ap.add_argument('--feedback', type=float, default=None,
                     help='inject this energy at each matched template (ros_simulate.py:107-108)')
     ap.add_argument('--gpus', type=int, default=1,
-                    help='ranks under torch.distributed.run: the template library is sharded '
-                         'over them, the pose cells are replicated')
-    ap.add_argument('--gloo', action='store_true',
+                    help='ranks (launched here, or by torch.distributed.run): the template '
+                         'library is sharded over them, the pose cells are replicated')
+    ap.add_argument('--host-reduce', action='store_true',
                     help='combine the ranks\' keys on the host (several ranks on one GPU)')
     args = ap.parse_args(argv)
+    from . import launch
+    if args.gpus > 1 and not launch.under_launcher():
+        return launch.spawn(args.gpus, ['-m', 'pyratslam_amd.replay'] + list(
+            sys.argv[1:] if argv is None else argv))
     from .dist import Dist
     d = Dist(args.gpus)
     dev = d.local if args.device is None else args.device
-    vts = sharded_templates(d, dev, args.gloo) if d.world > 1 else None
+    vts = sharded_templates(d, dev, args.host_reduce) if d.world > 1 else None
     r = RatslamReplay(device=dev, precision=args.precision, feedback_energy=args.feedback, vts=vts)
     d.barrier()
     t0 = time.perf_counter()

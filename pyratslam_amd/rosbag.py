@@ -298,8 +298,9 @@ def encode_image(stamp, pixels, encoding='mono8', frame_id=b'camera'):
 
 def image_to_mono8(img):
     """``bridge.imgmsg_to_cv(data, "mono8")`` then ``asarray`` (ros_simulate.py:100-101):
-    (height, width) uint8.  mono8 passes through; 8-bit colour converts with the
-    ITU-R 601 luma weights OpenCV's RGB->GRAY uses, rounded to nearest."""
+    (height, width) uint8.  mono8 passes through; 8-bit colour converts as
+    cv_bridge does (OpenCV cvtColor RGB2GRAY on 8-bit data): the ITU-R 601 luma
+    weights in 14-bit fixed point, (4899 R + 9617 G + 1868 B + 2^13) >> 14."""
     buf = np.frombuffer(img.data, dtype=np.uint8)
     if img.encoding in ('mono8', '8UC1'):
         rows = buf.reshape(img.height, img.step)[:, :img.width]
@@ -309,6 +310,7 @@ def image_to_mono8(img):
         px = buf.reshape(img.height, img.step)[:, :img.width * ch].reshape(img.height, img.width, ch)
         r, g, b = (px[..., 0], px[..., 1], px[..., 2]) if img.encoding.startswith('rgb') else \
                   (px[..., 2], px[..., 1], px[..., 0])
-        y = 0.299 * r + 0.587 * g + 0.114 * b
-        return np.clip(np.floor(y + 0.5), 0, 255).astype(np.uint8)
+        y = (4899 * r.astype(np.uint32) + 9617 * g.astype(np.uint32) + 1868 * b.astype(np.uint32)
+             + (1 << 13)) >> 14
+        return y.astype(np.uint8)
     raise BagError('image encoding %r is not supported for mono8 conversion' % img.encoding)

@@ -11,8 +11,13 @@ threshold / first-argmin / append-on-miss rule.  ``match_batch`` runs many
 matches with the exact sequential semantics in one call.
 ``ShardedViewTemplates`` spreads the library over ranks (one GPU each).
 
-Frames must be ``uint8`` (the ROS path, ``ros_simulate.py:100-101``); the
-subsampling mask is the reference's, with Python-2 integer division (:44-54).
+Frames are ``uint8`` on the ROS path (``ros_simulate.py:100-101``): the library
+then lives on the GPU and a score wraps mod 256 like numpy's uint8 subtraction.
+float32 / float64 frames follow the reference's float semantics instead (a true
+sum of |T - Q| in numpy's summation order, ``rs_sad_scores`` on the GPU): once a
+float frame is matched the library is scored pair-wise per match (a fidelity
+path for float callers, not the throughput path).  The subsampling mask is the
+reference's, with Python-2 integer division (:44-54).
 """
 import ctypes
 import threading
@@ -22,6 +27,41 @@ import numpy as np
 from . import _lib
 
 MAX_OFFSET = 8  # view_templates.py:14
+_FLOAT_CODES = {np.dtype(np.float32): _lib.RS_DT_F32, np.dtype(np.float64): _lib.RS_DT_F64}
+
+
+def sad_scores(templates, queries, max_offset=MAX_OFFSET, device=0):
+    """``ViewTemplate.match`` (view_templates.py:16-28) of every (query, template)
+    pair of float arrays on the GPU: (nq, nt) scores in numpy's result dtype of the
+    two arrays (float32 or float64), bit-exact to the reference's numpy arithmetic."""
+    t = np.asarray(templates)
+    q = np.asarray(queries)
+    dt = np.result_type(t.dtype, q.dtype)
+    if dt not in _FLOAT_CODES:
+        raise TypeError('ViewTemplate.match takes uint8 (wrapping) or float32/float64 arrays; '
+                        'got %s and %s' % (t.dtype, q.dtype))
+    if t.ndim != 3 or q.ndim != 3 or t.shape[1:] != q.shape[1:]:
+        raise ValueError('template / query shapes %r, %r differ' % (t.shape[1:], q.shape[1:]))
+    t = np.ascontiguousarray(t, dtype=dt)
+    q = np.ascontiguousarray(q, dtype=dt)
+    out = np.empty((q.shape[0], t.shape[0]), dtype=dt)
+    lib = _lib.require_device()
+    _lib.check(lib.rs_sad_scores(int(device), _FLOAT_CODES[dt], t.shape[1], t.shape[2], int(max_offset),
+                                 t.shape[0], ctypes.c_void_p(t.ctypes.data), q.shape[0],
+                                 ctypes.c_void_p(q.ctypes.data), ctypes.c_void_p(out.ctypes.data)))
+    return out
+
+
+def _wrapped_scores(templates, queries, device=0):
+    """uint8 pair scores through a temporary device library (float-mode libraries
+    that also hold uint8 templates)."""
+    t = np.ascontiguousarray(templates, dtype=np.uint8)
+    lib = ViewTemplates._from_shape(t.shape[1:], np.inf, device=device, capacity=len(t))
+    try:
+        lib.add(t)
+        return lib.scores(queries)
+    finally:
+        lib.close()
 
 
 def py2_mask(x_range, y_range, x_step, y_step, im_x, im_y):
@@ -48,13 +88,25 @@ class ViewTemplate:
         self._solo = None
 
     def match(self, new_template):
-        """Row-shift score against ``new_template`` (view_templates.py:16-28), on the GPU."""
+        """Row-shift score against ``new_template`` (view_templates.py:16-28), on the
+        GPU: uint8 arrays wrap mod 256 (numpy uint8 arithmetic, a numpy.uint64
+        score); float arrays give numpy's true sum of |T - Q| in their dtype."""
+        if self.template is None:
+            owner = self._owner
+            raise ValueError('the bytes of template %d live on rank %d (template g is stored on '
+                             'rank g %% %d): score it there' % (self.index, self.index % owner.nranks,
+                                                                owner.nranks))
         q = np.ascontiguousarray(new_template)
-        if self._owner is not None and self._owner.nranks == 1:
-            return self._owner.scores(q[None], self.index, 1)[0, 0]
+        t = np.asarray(self.template)
+        dev = self._owner.device if self._owner is not None else 0
+        if t.dtype != np.uint8 or q.dtype != np.uint8:
+            return sad_scores(t[None], q[None], self.max_offset, dev)[0, 0]
+        owner = self._owner
+        if owner is not None and owner.nranks == 1 and not owner._float:
+            return owner.scores(q[None], self.index, 1)[0, 0]
         if self._solo is None:
-            t = np.ascontiguousarray(self.template)
-            self._solo = ViewTemplates._from_shape(t.shape, np.iinfo(np.uint64).max)
+            t = np.ascontiguousarray(t)
+            self._solo = ViewTemplates._from_shape(t.shape, np.inf, device=dev)
             self._solo.add(t[None])
         return self._solo.scores(q[None], 0, 1)[0, 0]
 
@@ -87,17 +139,17 @@ class ViewTemplates:
         self.templates = []
         self.device = int(device)
         self.rank, self.nranks = 0, 1
+        self._float = False      # float frames seen: pair-wise float scoring (module doc)
         self._mutex = threading.Lock()
         self._h = None
         self._lib = _lib.require_device()
-        # scores are integers, so `score > t` == `score > floor(t)` (view_templates.py:67)
-        if not match_threshold >= 0:
-            raise ValueError('match_threshold must be >= 0, got %r' % (match_threshold,))
-        thr = min(int(np.floor(match_threshold)), int(np.iinfo(np.uint64).max))
         h = ctypes.c_void_p()
-        _lib.check(self._lib.rs_vt_create(self.shape[0], self.shape[1], MAX_OFFSET, thr,
+        _lib.check(self._lib.rs_vt_create(self.shape[0], self.shape[1], MAX_OFFSET, 0,
                                           int(capacity), self.device, ctypes.byref(h)))
         self._h = h
+        # `min(match_val) > match_threshold` (view_templates.py:67), compared in float64 as
+        # numpy compares the uint64 score with a Python number (inf: never, < 0: always)
+        _lib.check(self._lib.rs_vt_set_threshold(h, float(match_threshold)))
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
@@ -121,9 +173,9 @@ class ViewTemplates:
     def subsample(self, image):
         """``input[self.mask].reshape(self.shape)`` (view_templates.py:64)."""
         im = np.asarray(image)
-        if im.dtype != np.uint8:
-            raise TypeError('ViewTemplates matches uint8 frames (mono8, ros_simulate.py:100-101); '
-                            'got %s' % im.dtype)
+        if im.dtype != np.uint8 and im.dtype not in _FLOAT_CODES:
+            raise TypeError('ViewTemplates matches uint8 (mono8, ros_simulate.py:100-101) or '
+                            'float32/float64 frames; got %s' % im.dtype)
         if im.shape != self.mask.shape:
             raise ValueError('frame shape %r does not match the mask %r' % (im.shape, self.mask.shape))
         return im[self.mask].reshape(self.shape)
@@ -177,6 +229,8 @@ class ViewTemplates:
     def match_templates(self, queries, pcs=None, mode=_lib.RS_VT_SEQUENTIAL):
         """Match already-subsampled (nq, H, W) queries; returns (index, score, is_new)."""
         q = self._check_templates(queries)
+        if self._float:
+            raise TypeError('this library has matched float frames: use match() / match_batch()')
         n = q.shape[0]
         idx = np.empty(n, dtype=np.int64)
         score = np.empty(n, dtype=np.uint64)
@@ -220,14 +274,46 @@ class ViewTemplates:
     def match(self, input, pc_x, pc_y, pc_th):
         """Best template for a frame, or a new one (view_templates.py:63-75)."""
         t = self.subsample(input)
+        if t.dtype != np.uint8 or self._float:
+            return self._match_float(t, (pc_x, pc_y, pc_th))
         idx, _, _ = self.match_templates(t[None], [(pc_x, pc_y, pc_th)])
         return self.templates[int(idx[0])]
 
     def match_batch(self, images, pcs):
         """``[match(im, *pc) for im, pc in zip(images, pcs)]`` in one call."""
-        q = np.stack([self.subsample(im) for im in images])
-        idx, _, _ = self.match_templates(q, pcs)
+        q = [self.subsample(im) for im in images]
+        if self._float or any(x.dtype != np.uint8 for x in q):
+            return [self._match_float(x, pc) for x, pc in zip(q, pcs)]
+        idx, _, _ = self.match_templates(np.stack(q), pcs)
         return [self.templates[int(i)] for i in idx]
+
+    def _match_float(self, template, pc):
+        """ViewTemplates.match (view_templates.py:63-75) on the float path: every
+        stored template scored on the GPU in numpy's dtype of the pair, then the
+        reference's own rule -- builtin min over the list against the threshold,
+        numpy argmin for the best."""
+        if self.nranks > 1:
+            raise TypeError('float frames are not supported by a sharded library')
+        with self._mutex:
+            self._float = True
+            match_val = [None] * len(self.templates)
+            groups = {}
+            for i, tm in enumerate(self.templates):
+                groups.setdefault(np.asarray(tm.template).dtype, []).append(i)
+            for dt, ids in groups.items():
+                lib = np.stack([np.asarray(self.templates[i].template) for i in ids])
+                if dt == np.uint8 and template.dtype == np.uint8:
+                    sc = _wrapped_scores(lib, template[None], self.device)[0]
+                else:
+                    sc = sad_scores(lib, template[None], MAX_OFFSET, self.device)[0]
+                for i, v in zip(ids, sc):
+                    match_val[i] = v
+            if len(match_val) == 0 or min(match_val) > self.match_threshold:
+                new = ViewTemplate(pc[0], pc[1], pc[2], len(self.templates), np.array(template),
+                                   _owner=self)
+                self.templates.append(new)
+                return new
+            return self.templates[int(np.argmin(match_val))]
 
     # -- on-device subsampling --------------------------------------------------
     def _ensure_gather(self):

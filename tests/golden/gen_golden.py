@@ -372,6 +372,46 @@ def gen_templates(vt, out):
     trace('vt_trace_64x32', 160, (16, 144), (16, 80), 2, 45000, 300, 6, 3)
 
 
+def gen_float_pairs(vt, out):
+    """ViewTemplate.match / ViewTemplates.match on float frames (view_templates.py:
+    16-28, 63-75): no uint8 wrap, numpy's own float arithmetic and summation order.
+    Non-integer values, float64 and float32, H in {64, 32, 24}; plus a library
+    trace through the unmodified ViewTemplates.match with float64 frames."""
+    rng = np.random.default_rng(11)
+    arrays = {}
+    for i, (h, w) in enumerate(((64, 32), (32, 32), (24, 20))):
+        for dt, tag in ((np.float64, 'f64'), (np.float32, 'f32')):
+            a = (rng.random((16, h, w)) * 255).astype(dt)
+            b = (rng.random((16, h, w)) * 255).astype(dt)
+            for j in range(8):   # half: shifted noisy copies (scores near the minimum)
+                sh = int(rng.integers(-7, 8))
+                b[j] = (np.roll(a[j], sh, axis=0) + rng.normal(0, 3, (h, w))).astype(dt)
+            s = np.array([vt.ViewTemplate(0, 0, 0, 0, a[j]).match(b[j]) for j in range(16)])
+            assert s.dtype == dt, (s.dtype, dt)
+            arrays.update({f'{tag}_{i}_a': a, f'{tag}_{i}_b': b, f'{tag}_{i}_score': s})
+    # float64 frames normalised to [0, 1] (a camera pipeline that scales), ROS geometry
+    r = np.random.default_rng(12)
+    vts = vt.ViewTemplates(x_range=(32, 96), y_range=(32, 96), x_step=Py2Int(2), y_step=Py2Int(2),
+                           im_x=256, im_y=256, match_threshold=45000 / 255.0)
+    vts.shape = tuple(int(s) for s in vts.shape)
+    vts.mask = np.asarray(vts.mask, dtype=bool).view(np.ndarray)
+    bases = r.random((10, 256, 256))
+    frames, idx = [], []
+    for k in range(60):
+        if r.random() < 0.75:
+            f = np.roll(bases[int(r.integers(0, 10))], 2 * int(r.integers(-5, 6)), axis=0)
+            f = f + r.normal(0, 0.01 if r.random() < 0.7 else 0.2, f.shape)
+        else:
+            f = r.random((256, 256))
+        frames.append(f)
+        idx.append(vts.match(f, k % 21, (3 * k) % 21, (5 * k) % 36).get_index())
+    arrays.update(trace_queries=np.stack([f[vts.mask].reshape(vts.shape) for f in frames]),
+                  trace_index=np.array(idx), trace_threshold=np.array(45000 / 255.0),
+                  trace_templates=np.stack([t.template for t in vts.templates]))
+    np.savez_compressed(os.path.join(out, 'vt_pairs_float.npz'), **arrays)
+    print('float pairs: %d templates in the float trace' % len(vts.templates))
+
+
 def gen_ros_replay(pn, vt, out, n=120, seed=0):
     """Config 5 end to end with the reference's own classes: PoseCellNetwork,
     ViewTemplates and ExperienceMap (experience_map.py, imported unmodified)
@@ -403,7 +443,8 @@ def gen_ros_replay(pn, vt, out, n=120, seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default=os.path.dirname(os.path.abspath(__file__)))
-    ap.add_argument('--only', choices=['kernels', 'posecell', 'templates', 'ros_replay'])
+    ap.add_argument('--only', choices=['kernels', 'posecell', 'templates', 'float_pairs',
+                                       'ros_replay'])
     args = ap.parse_args()
     pn, vt = load_reference()
     if args.only in (None, 'kernels'):
@@ -412,6 +453,8 @@ def main():
         gen_posecell(pn, args.out)
     if args.only in (None, 'templates'):
         gen_templates(vt, args.out)
+    if args.only in (None, 'float_pairs'):
+        gen_float_pairs(vt, args.out)
     if args.only in (None, 'ros_replay'):
         gen_ros_replay(pn, vt, args.out)
     print('golden vectors written to', args.out)

@@ -1,91 +1,122 @@
-"""N>1 host orchestration on CPU with torch.distributed gloo, world size 2.
+"""N>1 host orchestration on CPU, no PyTorch in the path: the launcher
+(pyratslam_amd.launch, what ``python bench.py --gpus N`` uses) and the TCP
+control plane (pyratslam_amd.dist) at world sizes 2 and 3, and the same control
+plane under torch.distributed.run (the driver's launcher for the scaling bench).
 
-Covers what runs on every rank besides the GPU scan: bench.py's control plane
-(barrier, RCCL unique-id broadcast, max-over-ranks time, the host uint64 min
-reducer with UINT64_MAX = "no template") and the sharding protocol of
+Covers what runs on every rank besides the GPU scan: barriers, the RCCL
+unique-id broadcast, the max-over-ranks time, the host uint64 min reducer
+(unsigned order, UINT64_MAX = "no template") and the sharding protocol of
 ShardedViewTemplates -- template g on rank g % n at slot g // n, packed keys
 (score << 32 | g), elementwise min over ranks == the unsharded first argmin.
-The per-rank scan is played by the oracle here (test infrastructure); on the
-GPU it is rs_vt_scan_local, checked against the same protocol in
-tests/test_view_templates_gpu.py::test_sharded_ranks_simulated_on_one_gpu.
+The per-rank scan is played by the oracle (tests/_dist_worker.py); on the GPU
+it is rs_vt_scan_local (tests/test_view_templates_gpu.py, test_sharded_*).
 """
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 
-torch = pytest.importorskip('torch')
-import torch.distributed as dist  # noqa: E402
-import torch.multiprocessing as mp  # noqa: E402
-
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NO_KEY = np.iinfo(np.uint64).max
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _env():
+    env = dict(os.environ)
+    for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_PORT', 'RS_DIST_DIR'):
+        env.pop(k, None)
+    return env
 
 
-def _local_keys(shard, gids, queries):
-    from oracle import view_templates as V
-    keys = np.full(len(queries), NO_KEY, dtype=np.uint64)
-    if len(shard) == 0:
-        return keys
-    for i, q in enumerate(queries):
-        sc = V.vt_scores_library(shard, q)
-        k = (sc.astype(np.uint64) << np.uint64(32)) | gids.astype(np.uint64)
-        keys[i] = k.min()
-    return keys
+def _json_line(r):
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
+    return json.loads(lines[-1])
 
 
-def _worker(rank, world, port, out):
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, root)
-    import bench
-    from pyratslam_amd import synthetic
-    d = bench.Dist(world)
-    try:
-        d.barrier()
-        uid = d.bcast_bytes(b'rank0-unique-id' if rank == 0 else None)
-        assert uid == b'rank0-unique-id'
-        assert d.max(float(rank) + 0.5) == world - 0.5
-        lib = synthetic.library(48, seed=7)
-        qs, src = synthetic.queries(lib, 24, seed=8, hit_frac=0.75)
-        gids = np.arange(rank, len(lib), world)          # template g on rank g % world
-        local = _local_keys(lib[gids], gids, qs)
-        glob = d.min_keys(local)
-        out[rank] = glob.copy()
-        # "no template" (UINT64_MAX) survives the signed int64 gloo reduction
-        probe = np.array([NO_KEY, 5, NO_KEY, (1 << 40) | 3], dtype=np.uint64)
-        if rank == 1:
-            probe = np.array([NO_KEY, NO_KEY, 7, (1 << 40) | 1], dtype=np.uint64)
-        out['probe%d' % rank] = d.min_keys(probe).copy()
-    finally:
-        d.close()
-
-
-def test_sharded_min_reduce_gloo_world2():
+def _check_protocol(out, world):
     from oracle import view_templates as V
     from pyratslam_amd import synthetic
-    world = 2
-    port = _free_port()
-    mgr = mp.Manager()
-    out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    assert np.array_equal(out[0], out[1])
-    expect = np.array([NO_KEY, 5, 7, (1 << 40) | 1], dtype=np.uint64)
-    assert np.array_equal(out['probe0'], expect) and np.array_equal(out['probe1'], expect)
+    assert out['world'] == world
+    expect = [NO_KEY, 5, 1 << 63, (1 << 40) | (3 - (world - 1))]
+    assert out['probe'] == [int(v) for v in expect]
     lib = synthetic.library(48, seed=7)
     qs, _ = synthetic.queries(lib, 24, seed=8, hit_frac=0.75)
     for i, q in enumerate(qs):
         sc = V.vt_scores_library(lib, q)
-        key = int(out[0][i])
+        key = out['keys'][i]
         assert key >> 32 == int(sc.min())
         assert key & 0xFFFFFFFF == int(np.argmin(sc))
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_launcher_and_control_plane(world):
+    code = ('import sys; sys.path.insert(0, %r); from pyratslam_amd import launch; '
+            'sys.exit(launch.spawn(%d, [%r]))' % (ROOT, world, os.path.join(ROOT, 'tests', '_dist_worker.py')))
+    r = subprocess.run([sys.executable, '-c', code], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=120)
+    _check_protocol(_json_line(r), world)
+
+
+def test_control_plane_under_torchrun():
+    pytest.importorskip('torch')
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(port),
+           os.path.join(ROOT, 'tests', '_dist_worker.py')]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=180)
+    _check_protocol(_json_line(r), 2)
+
+
+def test_dist_selftest_and_failure_propagates():
+    """dist's own self-test through the launcher; a failing rank fails the job
+    (and the launcher ends the rank left waiting for it)."""
+    code = ('import sys; sys.path.insert(0, %r); from pyratslam_amd import launch; '
+            'sys.exit(launch.spawn(2, ["-m", "pyratslam_amd.dist"]))' % ROOT)
+    r = subprocess.run([sys.executable, '-c', code], cwd=ROOT, env=_env(), capture_output=True,
+                       text=True, timeout=120)
+    out = _json_line(r)
+    assert out['world'] == 2 and out['uid'] == 'unique-id-of-rank-0' and out['max'] == 1.5
+    assert out['min_keys'] == [int(NO_KEY), 5, 1 << 63, (3 << 32) | 6]
+    bad = ('import os, sys; sys.path.insert(0, %r)\n'
+           'from pyratslam_amd.dist import Dist\n'
+           'd = Dist()\n'
+           'if d.rank == 1: sys.exit(3)\n'
+           'd.barrier()\n' % ROOT)
+    path = os.path.join(ROOT, 'tests', '.fail_rank.py')
+    with open(path, 'w') as f:
+        f.write(bad)
+    try:
+        code = ('import sys; sys.path.insert(0, %r); from pyratslam_amd import launch; '
+                'sys.exit(launch.spawn(2, [%r]))' % (ROOT, path))
+        r = subprocess.run([sys.executable, '-c', code], cwd=ROOT, env=_env(), capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode != 0
+    finally:
+        os.unlink(path)
+
+
+def test_bench_spawns_its_own_ranks(monkeypatch):
+    """``python bench.py --gpus N`` hands off to launch.spawn before touching the GPU."""
+    import bench
+    from pyratslam_amd import launch
+    for k in ('RANK', 'WORLD_SIZE'):
+        monkeypatch.delenv(k, raising=False)
+    seen = {}
+
+    def fake_spawn(n, argv, **kw):
+        seen['n'], seen['argv'] = n, argv
+        return 0
+    monkeypatch.setattr(launch, 'spawn', fake_spawn)
+    monkeypatch.setattr(sys, 'argv', ['bench.py', '--gpus', '4', '--steps', '3'])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0
+    assert seen['n'] == 4 and seen['argv'][0].endswith('bench.py') and seen['argv'][1:] == [
+        '--gpus', '4', '--steps', '3']

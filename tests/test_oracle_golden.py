@@ -109,3 +109,33 @@ def test_c_oracle_matches_reference():
     for i, q in enumerate(qs):
         ref = V.vt_scores_library(lib, q)
         assert sc[i] == ref.min() and ix[i] == np.argmin(ref)
+
+
+@pytest.mark.parametrize('tag', ['f64', 'f32'])
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_vt_float_pair_scores_bit_exact(tag, i):
+    """Float frames (view_templates.py:16-28 without the uint8 wrap): the reference's
+    own scores on non-integer float64 / float32 data (tests/golden: float_pairs)."""
+    d = load_golden('vt_pairs_float')
+    a, b, s = d[f'{tag}_{i}_a'], d[f'{tag}_{i}_b'], d[f'{tag}_{i}_score']
+    assert s.dtype == a.dtype
+    for j in range(len(a)):
+        got = V.vt_score(a[j], b[j])
+        assert got == s[j] and np.asarray(got).dtype == s.dtype
+
+
+def test_vt_float_trace_bit_exact():
+    """ViewTemplates.match with float64 frames through the reference's rule (builtin
+    min against the threshold, numpy argmin): the oracle replays the golden trace."""
+    d = load_golden('vt_pairs_float')
+    thr = float(d['trace_threshold'])
+    lib = []
+    for q, want in zip(d['trace_queries'], d['trace_index']):
+        vals = [V.vt_score(t, q) for t in lib]
+        if not vals or min(vals) > thr:
+            lib.append(q)
+            got = len(lib) - 1
+        else:
+            got = int(np.argmin(vals))
+        assert got == want
+    assert np.array_equal(np.stack(lib), d['trace_templates'])

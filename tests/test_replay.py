@@ -83,10 +83,16 @@ def test_colour_frames_to_mono8():
     rgb = np.random.default_rng(0).integers(0, 256, (5, 7, 3), dtype=np.uint8)
     img = rosbag.decode_image(rosbag.encode_image(2.0, rgb, encoding='rgb8'))
     got = rosbag.image_to_mono8(img)
-    want = np.floor(0.299 * rgb[..., 0] + 0.587 * rgb[..., 1] + 0.114 * rgb[..., 2] + 0.5)
+    # cv_bridge / OpenCV RGB2GRAY on 8-bit data: 14-bit fixed point, rounded
+    r, g, b = (rgb[..., i].astype(np.int64) for i in range(3))
+    want = (4899 * r + 9617 * g + 1868 * b + 8192) >> 14
     assert np.array_equal(got, want.astype(np.uint8))
     bgr = rosbag.decode_image(rosbag.encode_image(2.0, rgb[..., ::-1], encoding='bgr8'))
     assert np.array_equal(rosbag.image_to_mono8(bgr), got)
+    # OpenCV's known outputs for the primaries and white: 76, 150, 29, 255
+    prim = np.array([[[255, 0, 0], [0, 255, 0], [0, 0, 255], [255, 255, 255]]], dtype=np.uint8)
+    img = rosbag.decode_image(rosbag.encode_image(2.0, prim, encoding='rgb8'))
+    assert rosbag.image_to_mono8(img).tolist() == [[76, 150, 29, 255]]
 
 
 def test_clip_rad_180():

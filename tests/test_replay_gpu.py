@@ -65,23 +65,20 @@ def test_replay_cli_synthetic(capsys):
 
 
 def test_two_rank_sharded_replay(golden):
-    """Config 5 over ranks: the library sharded over two processes (one GPU box:
-    both on device 0 with the gloo key reducer; RCCL on a multi-GPU node), pose
-    cells replicated; rank 0's outputs equal the reference's."""
+    """Config 5 over ranks: the library sharded over two processes that the
+    replay launches itself (one GPU box: both on device 0 with the host key
+    reducer; RCCL on a multi-GPU node), pose cells replicated; rank 0's outputs
+    equal the reference's."""
     import json
     import os
-    import socket
     import subprocess
     import sys
-    s = socket.socket()
-    s.bind(('127.0.0.1', 0))
-    port = s.getsockname()[1]
-    s.close()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', str(port), '-m', 'pyratslam_amd.replay',
-           '--synthetic', str(int(golden['n'])), '--gpus', '2', '--gloo', '--device', '0']
+    for k in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK'):
+        env.pop(k, None)
+    cmd = [sys.executable, '-m', 'pyratslam_amd.replay', '--synthetic', str(int(golden['n'])),
+           '--gpus', '2', '--host-reduce', '--device', '0']
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=150)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
     assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]

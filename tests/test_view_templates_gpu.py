@@ -81,10 +81,10 @@ def test_frozen_scan_vs_oracle(vtmod, t, q, h, w):
     assert len(lib.templates) == t
 
 
-@pytest.mark.parametrize('scan', ['plane', 'carry', 'sad', 'rb2', 'rb3'])
+@pytest.mark.parametrize('scan', ['plane', 'carry'])
 @pytest.mark.parametrize('h', [64, 32])
 def test_scan_variants_vs_oracle(vtmod, monkeypatch, scan, h):
-    """Every scan form (RS_VT_SCAN; 'plane' is the default bit-plane scan) gives
+    """Both scan forms (RS_VT_SCAN; 'plane' is the default bit-plane scan) give
     the oracle's scores on the same inputs, including all-0 / all-255 extremes."""
     monkeypatch.setenv('RS_VT_SCAN', scan)
     rng = np.random.default_rng(h)
@@ -238,11 +238,99 @@ def test_sharded_python_reducer_path(vtmod):
 def test_type_and_shape_errors(vtmod):
     vts = vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, 45000)
     with pytest.raises(TypeError):
-        vts.match(np.zeros((256, 256), dtype=np.float32), 0, 0, 0)
+        vts.match(np.zeros((256, 256), dtype=np.int16), 0, 0, 0)
     with pytest.raises(ValueError):
         vts.match(np.zeros((128, 128), dtype=np.uint8), 0, 0, 0)
-    with pytest.raises(ValueError):
-        vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, -1)
+    with pytest.raises(TypeError):
+        vtmod.sad_scores(np.zeros((1, 32, 32), np.int32), np.zeros((1, 32, 32), np.int32))
+
+
+@pytest.mark.parametrize('thr', [-1, -0.5, float('inf'), float('nan'), 2 ** 70, 0, 0.999, 5])
+def test_threshold_rule_like_numpy(vtmod, thr):
+    """`min(match_val) > match_threshold` (view_templates.py:67) for any Python number,
+    compared as numpy compares the uint64 score: a negative threshold always appends,
+    inf / NaN / huge never do, an exact copy (score 0) is a hit for any threshold >= 0."""
+    t = V.synthetic_library(4, 32, 32, seed=3)
+    lib = vtmod.ViewTemplates._from_shape((32, 32), thr)
+    lib.add(t)
+    idx, score, new = lib.match_templates(t)      # exact copies, score 0
+    assert (score == 0).all()
+    expect = bool(np.uint64(0) > thr)
+    assert list(new) == [expect] * 4
+    if not expect:
+        assert list(idx) == [0, 1, 2, 3]
+    q = V.synthetic_library(1, 32, 32, seed=99)   # unrelated frame: a large score
+    _, sc, new = lib.match_templates(q)
+    assert bool(new[0]) == bool(np.uint64(sc[0]) > thr)
+
+
+def test_pair_score_of_one_template_scans_only_its_block(vtmod):
+    """ViewTemplate.match on an owned template scores [t0, t0 + 1) only (no whole-
+    library scan): right score for templates in every 64-slot block, and the staged
+    match batch is not mistaken for the scored query."""
+    import ctypes
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(300, 64, 32, seed=51)
+    q, _ = V.synthetic_queries(lib_np, 3, seed=52)
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    lib.add(lib_np)
+    lib.match_templates(q, mode=0)                 # stages q
+    for t in (0, 63, 64, 200, 299):
+        assert lib.templates[t].match(q[1]) == V.vt_score(lib_np[t], q[1])
+    sc = lib.scores(q, 130, 7)
+    assert np.array_equal(sc, np.stack([V.vt_scores_library(lib_np[130:137], x) for x in q]))
+    with pytest.raises(RuntimeError):             # the staged batch was replaced by scores()
+        _lib.check(lib._lib.rs_vt_resolve(lib._h, 3, _lib.ptr(np.zeros(3, np.uint64), ctypes.c_uint64),
+                                          1, None, None, None))
+
+
+def test_template_bytes_on_another_rank_raise(vtmod):
+    t = vtmod.ViewTemplate(0, 0, 0, 5, None, _owner=vtmod.ShardedViewTemplates.from_shape(
+        (32, 32), 45000, 0, 2, reducer=lambda k: k))
+    with pytest.raises(ValueError, match='rank 1'):
+        t.match(np.zeros((32, 32), np.uint8))
+
+
+@pytest.mark.parametrize('tag', ['f64', 'f32'])
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_float_pair_scores_bit_exact(vtmod, tag, i):
+    """Float ViewTemplate.match on the GPU (rs_sad_scores: true SAD in the arrays'
+    dtype, numpy's pairwise summation order) equals the reference's scores bit for
+    bit on non-integer float64 / float32 data."""
+    d = load_golden('vt_pairs_float')
+    a, b, s = d[f'{tag}_{i}_a'], d[f'{tag}_{i}_b'], d[f'{tag}_{i}_score']
+    sc = vtmod.sad_scores(a, b)                   # (query, template)
+    assert sc.dtype == s.dtype
+    assert np.array_equal(np.diagonal(sc), s)
+    for j in (0, 9):
+        got = vtmod.ViewTemplate(0, 0, 0, j, a[j]).match(b[j])
+        assert got == s[j] and np.asarray(got).dtype == s.dtype
+
+
+@pytest.mark.parametrize('i', [0, 1, 2])
+def test_integer_valued_float_pairs(vtmod, i):
+    """uint8 pairs cast to float64 (the golden f64 scores): true SAD, no wrap."""
+    d = load_golden('vt_pairs')
+    a, b = d[f'u8_{i}_a'].astype(np.float64), d[f'u8_{i}_b'].astype(np.float64)
+    assert np.array_equal(np.diagonal(vtmod.sad_scores(a, b)), d[f'f64_{i}_score'])
+    mixed = vtmod.ViewTemplate(0, 0, 0, 0, d[f'u8_{i}_a'][4]).match(b[4])   # uint8 x float64
+    assert mixed == d[f'f64_{i}_score'][4]
+
+
+def test_float_frames_trace(vtmod):
+    """ViewTemplates.match with float64 frames reproduces the reference's trace."""
+    d = load_golden('vt_pairs_float')
+    vts = vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, float(d['trace_threshold']))
+    for k, q in enumerate(d['trace_queries']):
+        t = vts.match(_float_frame(vts.mask, q), k % 21, (3 * k) % 21, (5 * k) % 36)
+        assert t.get_index() == d['trace_index'][k]
+    assert np.array_equal(np.stack([t.template for t in vts.templates]), d['trace_templates'])
+
+
+def _float_frame(mask, template):
+    im = np.zeros(mask.shape, dtype=np.float64)
+    im[mask] = template.ravel()
+    return im
 
 
 def test_library_growth(vtmod):
