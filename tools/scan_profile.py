@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Minimal workloads for rocprofv3 passes (tools/profile_r2.sh): one template
+configuration's frozen scans, or one pose-cell grid's batched steps, and nothing
+else, so every dispatch of the profiled kernel belongs to that configuration.
+
+usage: python tools/scan_profile.py scan --templates 1000 --queries 1024 --launches 20
+       python tools/scan_profile.py pc --shape 128,128,72 --steps 400
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def scan(a):
+    from pyratslam_amd import _lib, synthetic
+    from pyratslam_amd.view_templates import ViewTemplates
+    vts = ViewTemplates._from_shape((64, 32), 45000, capacity=a.templates)
+    for lo in range(0, a.templates, 8192):
+        vts.add(synthetic.library(min(8192, a.templates - lo), seed=1, first=lo))
+    qlib = synthetic.library(min(a.templates, 4096), seed=1)
+    qs, src = synthetic.queries_fast(qlib, a.queries, seed=2)
+    idx, _, _ = vts.match_templates(qs, mode=_lib.RS_VT_FROZEN)
+    ok = bool(np.all(idx[src >= 0] == src[src >= 0]))
+    ms = []
+    for _ in range(a.launches):
+        vts.match_templates(qs, mode=_lib.RS_VT_FROZEN)
+        ms.append(vts.device_ms())
+    print(json.dumps({'templates': a.templates, 'queries': a.queries, 'form': vts.scan_form(),
+                      'scan_ms': float(np.mean(ms)), 'hits_correct': ok}), flush=True)
+
+
+def pc(a):
+    from pyratslam_amd import PoseCellNetwork, synthetic
+    shape = tuple(int(s) for s in a.shape.split(','))
+    net = PoseCellNetwork(shape)
+    net.inject(1, tuple(s // 2 for s in shape))
+    od = synthetic.odometry(a.steps, seed=0)
+    net.run(od)
+    print(json.dumps({'shape': shape, 'form': net.step_form(),
+                      'finite': bool(np.isfinite(net.posecells).all())}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest='what', required=True)
+    s = sub.add_parser('scan')
+    s.add_argument('--templates', type=int, default=1000)
+    s.add_argument('--queries', type=int, default=1024)
+    s.add_argument('--launches', type=int, default=20)
+    p = sub.add_parser('pc')
+    p.add_argument('--shape', default='64,64,36')
+    p.add_argument('--steps', type=int, default=400)
+    a = ap.parse_args()
+    scan(a) if a.what == 'scan' else pc(a)
+
+
+if __name__ == '__main__':
+    main()
