@@ -348,90 +348,67 @@ __global__ __launch_bounds__(64) void vt_scan_generic_kernel(const uint4* __rest
 // i), and [T < Q] for all 32 pairs of a unit is the borrow out of T - Q,
 //   b = maj(~T_k, Q_k, b)  for k = 0..7   (one v_bitop3_b32 each, table 0x8E),
 // followed by one v_bcnt_u32_b32 into the offset's counter: 9 VALU per
-// 32 byte pairs.  Template unit J (rows 4J..4J+3) meets the query unit that
-// starts at row S (rows outside [M, H-M) zeroed: a zero byte never borrows) at
-// offset o = 4J - S; S runs over [M-3, H-M-1].
+// 32 byte pairs, against 3 per 4 pairs for the byte-SWAR forms above.
 //
-// Wave-local form: one wave owns TPW templates x all 4 column groups (x NH row
-// halves at H = 64): lane L = (h * 4 + cg) * TPW + t.  Every lane keeps the
-// template units its half of the start rows meets (NUH units x 8 planes) in
-// VGPRs, so the per-(query, offset) counts of a template meet only inside the
-// wave (permlane swaps + DPP): no cross-wave partials, no reducing waves.  The
-// halves start at rows SA(h) = 5 and 29 (both = 1 mod 4), so unit J - JLO(h)
-// meets start row SA(h) + i at the same offset in both halves, and one
-// compile-time-unrolled loop over i serves both (the half-0 rows past 28 and the
-// half-1 rows past H-M-1 are zero query planes).
-// A block of 64 / TPW waves covers one 64-slot template block and a contiguous
-// chunk of queries; each query's record (planes per lane group and row, then
-// QS) is copied HBM -> LDS by LDS-DMA one query ahead (double buffer, one
-// barrier per query); each wave's first-argmin key per query waits in LDS and
-// the block issues one atomicMin per query at its end.
+// Template planes: uint4 chunk ((((tb*CG + cg)*NU + j)*2 + g)*64 + t) holds
+// planes 4g..4g+3 of unit j (rows 4j..4j+3, columns 8cg..8cg+7) of slot
+// tb*64 + t.  TS: tsum[(tb*16 + o+M-1)*64 + t].
+// Query planes: for every start row s in [M-3, H-M-1] and column group cg, the
+// unit of rows s..s+3 with rows outside [M, H-M) zeroed (a zero byte never
+// borrows), qp[((q*CG + cg)*NS + s-(M-3))*8 + k]; qsum[q] = QS (raw bytes).
+//
+// A block is CG waves (one per column group) x 64 templates.  Wave cg keeps
+// its NU units x 8 planes in VGPRs and streams query planes through SGPRs
+// (wave-uniform scalar loads).  Template unit j meets query unit s at offset
+// o = 4j - s.  The CG partial counts per (query, offset, template) meet in LDS.
 // ===========================================================================
 constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
 
-#ifndef PL64_NH
-#define PL64_NH 2
+// Per-wave start/end stamps for the diagnostic probe (tools/vt_probe.hip defines
+// VT_STAMPS and the vt_dbg buffer): realtime (100 MHz), shader clock, hw ids.
+#ifdef VT_STAMPS
+#define VT_STAMP(slot)                                                                     \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0) {                                                     \
+            unsigned hw_, xcc_;                                                            \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
+            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6; \
+            d_[(slot) * 3 + 0] = __builtin_amdgcn_s_memrealtime();                         \
+            d_[(slot) * 3 + 1] = __builtin_amdgcn_s_memtime();                             \
+            d_[(slot) * 3 + 2] = ((unsigned long long)xcc_ << 32) | hw_;                   \
+        }                                                                                  \
+    } while (0)
+#else
+#define VT_STAMP(slot) \
+    do {               \
+    } while (0)
 #endif
-template <int H, int NH = (H == 64 ? PL64_NH : 1)> struct PlaneGeom;
-template <> struct PlaneGeom<64, 1> {   // all 51 start rows per lane: 16 units in VGPRs
-    static constexpr int NH = 1, NSH = 51, NUH = 16, TPW = 16, KPL = 4, WAVES = 3;
-    __host__ __device__ static constexpr int sa(int) { return 5; }
-    __host__ __device__ static constexpr int jlo(int) { return 0; }
-};
-template <> struct PlaneGeom<64, 2> {
-    static constexpr int NH = 2;    // row halves
-    static constexpr int NSH = 27;  // start rows per half: S = SA(h) + i, i < NSH
-    static constexpr int NUH = 10;  // template units held per lane
-    static constexpr int TPW = 8;   // templates per wave
-    static constexpr int KPL = 2;   // offsets per lane in the epilogue
-    static constexpr int WAVES = 4; // waves per SIMD the registers allow
-    __host__ __device__ static constexpr int sa(int h) { return h == 0 ? 5 : 29; }
-    __host__ __device__ static constexpr int jlo(int h) { return h == 0 ? 0 : 6; }
-};
-template <> struct PlaneGeom<32, 1> {
-    static constexpr int NH = 1, NSH = 19, NUH = 8, TPW = 16, KPL = 4, WAVES = 4;
-    __host__ __device__ static constexpr int sa(int) { return 5; }
-    __host__ __device__ static constexpr int jlo(int) { return 0; }
-};
-template <int H>
-struct PlaneDims : PlaneGeom<H> {
-    using G = PlaneGeom<H>;
-    static constexpr int M = FAST_M, NU = H / 4, NO = 2 * M - 1;
-    static constexpr int NG = G::NH * PL_CG;       // lane groups
-    static constexpr int WPB = 64 / G::TPW;        // waves per 64-slot block
-    static constexpr int S_HI = H - M - 1;         // last start row
-    static constexpr int QS_OFF = NG * G::NSH * 8;  // dword of QS in a query record
-    static constexpr int REC_DW = (QS_OFF + 1 + 255) / 256 * 256;  // record, whole KiB
-    static constexpr int NCHUNK = REC_DW / 256;    // LDS-DMA instructions per record
-    static constexpr int PL_U4 = WPB * G::NUH * 2 * 64;  // uint4 of planes per 64-slot block
-    static constexpr int TS_DW = WPB * G::KPL * 64;      // TS dwords per 64-slot block
-    static_assert(NG * G::TPW == 64 && G::KPL * NG >= NO, "lane / offset mapping");
-    static_assert(G::sa(0) == M - 3 && 4 * G::jlo(G::NH - 1) - G::sa(G::NH - 1) == -(M - 3),
-                  "halves must meet their units at equal offsets");
-};
+#ifndef PL_NB_Q
+#define PL_NB_Q 2
+#endif
+constexpr int PL_NB = PL_NB_Q;  // queries per LDS batch (staged planes; one reducing wave each)
 
-// One stored template: its planes, in the per-lane layout, and TS(o) per lane group.
-//   planes: uint4 at (((tb*WPB + wq)*NUH + j)*2 + g)*64 + L = planes 4g..4g+3 of unit
-//           JLO(h) + j (zero past the last unit), column group cg, of template
-//           slot tb*64 + wq*TPW + t, for lane L = (h*4 + cg)*TPW + t;
-//   tsv:    dword at ((tb*WPB + wq)*KPL + k)*64 + L = TS of offset index
-//           (h*4 + cg)*KPL + k (UINT32_MAX past the last offset).
-template <int H>
+__device__ inline uint32_t plane_borrows(const uint32_t (&t)[8], const uint32_t* q) {
+    uint32_t b = __builtin_amdgcn_bitop3_b32(t[0], q[0], 0u, 0x8E);
+#pragma unroll
+    for (int k = 1; k < 8; ++k) b = __builtin_amdgcn_bitop3_b32(t[k], q[k], b, 0x8E);
+    return b;
+}
+
+// One block per stored template: planes + TS of raw template src[t] into slot dst[t].
 __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __restrict__ raw,
                                                              const int32_t* __restrict__ src,
                                                              const int64_t* __restrict__ dst,
-                                                             uint4* __restrict__ planes,
-                                                             uint32_t* __restrict__ tsv) {
-    using D = PlaneDims<H>;
-    constexpr int W = 8 * PL_CG, NU = D::NU, M = D::M;
-    __shared__ uint32_t s_pl[NU][PL_CG][8];
-    __shared__ uint32_t s_row[H];
+                                                             int H, int M,
+                                                             uint32_t* __restrict__ planes,
+                                                             uint32_t* __restrict__ tsum) {
+    constexpr int W = 8 * PL_CG;
+    __shared__ uint32_t s_row[256];
     const uint8_t* T = raw + (size_t)src[blockIdx.x] * H * W;
     const int64_t slot = dst[blockIdx.x];
-    const int64_t tb = slot >> 6;
-    const int tl = (int)(slot & 63), wq = tl / D::TPW, t = tl % D::TPW;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31;
-    // 32 lanes per unit: lane i holds byte i; one ballot per bit plane
+    const int64_t tb = slot >> 6, tl = slot & 63;
+    const int NU = H / 4, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31;
     for (int u0 = 2 * wave; u0 < PL_CG * NU; u0 += 8) {
         const int u = u0 + (lane >> 5);
         const int cg = u / NU, j = u - cg * NU;
@@ -439,7 +416,9 @@ __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __re
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const unsigned long long m = __ballot((byte >> k) & 1u);
-            if (i == k && u < PL_CG * NU) s_pl[j][cg][k] = (uint32_t)(lane < 32 ? m : m >> 32);
+            if (i == k && u < PL_CG * NU)
+                planes[((((tb * PL_CG + cg) * NU + j) * 2 + (k >> 2)) * 64 + tl) * 4 + (k & 3)] =
+                    (uint32_t)(lane < 32 ? m : m >> 32);
         }
     }
     for (int r = threadIdx.x; r < H; r += blockDim.x) {
@@ -450,24 +429,12 @@ __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __re
         s_row[r] = acc;
     }
     __syncthreads();
-    const size_t base = (size_t)tb * D::WPB + wq;
-    for (int e = threadIdx.x; e < D::NG * D::NUH * 2; e += blockDim.x) {
-        const int g = e & 1, jj = (e >> 1) % D::NUH, grp = (e >> 1) / D::NUH;
-        const int h = grp / PL_CG, cg = grp % PL_CG, J = D::jlo(h) + jj;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (J < NU) v = make_uint4(s_pl[J][cg][4 * g], s_pl[J][cg][4 * g + 1], s_pl[J][cg][4 * g + 2],
-                                   s_pl[J][cg][4 * g + 3]);
-        planes[((base * D::NUH + jj) * 2 + g) * 64 + grp * D::TPW + t] = v;
-    }
-    for (int e = threadIdx.x; e < D::NG * D::KPL; e += blockDim.x) {
-        const int grp = e / D::KPL, k = e % D::KPL, oi = grp * D::KPL + k;
-        uint32_t ts = 0xFFFFFFFFu;
-        if (oi < D::NO) {
-            const int o = oi - (M - 1);
-            ts = 0;
+    if (threadIdx.x < 16) {
+        const int o = (int)threadIdx.x - (M - 1);
+        uint32_t ts = 0;
+        if (threadIdx.x < 2 * M - 1)
             for (int r = M + o; r < H - M + o; ++r) ts += s_row[r];
-        }
-        tsv[(base * D::KPL + k) * 64 + grp * D::TPW + t] = ts;
+        tsum[(tb * 16 + threadIdx.x) * 64 + tl] = ts;
     }
 }
 
@@ -485,6 +452,7 @@ __device__ inline void transpose8x8(uint32_t& lo, uint32_t& hi) {
 // 4x4 byte transpose: out[k] byte q = byte k of in[q].
 __device__ inline void transpose4x4_bytes(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                                           uint32_t (&o)[4]) {
+    // pairs: (a,b) -> byte k of a, byte k of b interleaved; likewise (c,d)
     const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u);  // a0 b0 a1 b1
     const uint32_t ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);  // a2 b2 a3 b3
     const uint32_t cd_lo = __builtin_amdgcn_perm(d, c, 0x05010400u);  // c0 d0 c1 d1
@@ -495,22 +463,21 @@ __device__ inline void transpose4x4_bytes(uint32_t a, uint32_t b, uint32_t c, ui
     o[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
 }
 
-// One block per query: its record of REC_DW dwords.  Phase 1: each thread
-// bit-transposes one 8-byte row segment (row r, column group cg) so byte k holds
-// bit k of its 8 pixels (rows outside [M, H-M) become zero) and adds the segment
-// to QS.  Phase 2: each thread assembles the unit of lane group (h, cg) at start
-// row S = SA(h) + i (zero where S belongs to the other half or lies past H-M-1):
-// plane k = byte k of its 4 segments, at dwords ((h*4 + cg)*NSH + i)*8.  Phase 3:
-// QS at QS_OFF, zero padding to the record's end.
-template <int H>
-__global__ __launch_bounds__(256) void vt_qrec_kernel(const uint8_t* __restrict__ raw,
-                                                      uint32_t* __restrict__ rec) {
-    using D = PlaneDims<H>;
-    constexpr int W = 8 * PL_CG, M = D::M;
+// One block per query: query planes for every start row, and QS.  Phase 1: each
+// thread bit-transposes one 8-byte row segment (row r, column group cg) so byte
+// k holds bit k of its 8 pixels (rows outside [M, H-M) become zero), and adds
+// the segment to QS.  Phase 2: each thread assembles one unit (4 rows from start
+// row S0 + si, column group cg): plane k = byte k of its 4 segments, two 16-byte
+// stores.  Bit b of plane k = bit k of pixel (row + b/8, col 8cg + b%8).
+__global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restrict__ raw, int H,
+                                                        int M, uint32_t* __restrict__ qp,
+                                                        uint32_t* __restrict__ qsum) {
+    constexpr int W = 8 * PL_CG;
     __shared__ uint32_t s_red[4];
-    __shared__ uint2 s_t[H * PL_CG];   // transposed segments
+    __shared__ uint2 s_t[64 * W / 8];   // transposed segments (H <= 64)
+    const int NS = H - 2 * M + 3, S0 = M - 3;
     const uint8_t* Q = raw + (size_t)blockIdx.x * H * W;
-    uint32_t* out = rec + (size_t)blockIdx.x * D::REC_DW;
+    uint32_t* out = qp + (size_t)blockIdx.x * PL_CG * NS * 8;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t part = 0;
     for (int d = threadIdx.x; d < H * W / 8; d += blockDim.x) {
@@ -522,17 +489,14 @@ __global__ __launch_bounds__(256) void vt_qrec_kernel(const uint8_t* __restrict_
         s_t[d] = live ? v : make_uint2(0u, 0u);
     }
     __syncthreads();
-    for (int u = threadIdx.x; u < D::NG * D::NSH; u += blockDim.x) {
-        const int grp = u / D::NSH, i = u - grp * D::NSH;
-        const int h = grp / PL_CG, cg = grp % PL_CG, S = D::sa(h) + i;
-        const bool valid = S <= D::S_HI && (h + 1 == D::NH || S < D::sa(h + 1));
-        uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
-        if (valid) {
-            const uint2 q0 = s_t[(S + 0) * PL_CG + cg], q1 = s_t[(S + 1) * PL_CG + cg];
-            const uint2 q2 = s_t[(S + 2) * PL_CG + cg], q3 = s_t[(S + 3) * PL_CG + cg];
-            transpose4x4_bytes(q0.x, q1.x, q2.x, q3.x, lo);
-            transpose4x4_bytes(q0.y, q1.y, q2.y, q3.y, hi);
-        }
+    const int NU = PL_CG * NS;
+    for (int u = threadIdx.x; u < NU; u += blockDim.x) {
+        const int cg = u / NS, r0 = S0 + (u - cg * NS);
+        const uint2 q0 = s_t[(r0 + 0) * PL_CG + cg], q1 = s_t[(r0 + 1) * PL_CG + cg];
+        const uint2 q2 = s_t[(r0 + 2) * PL_CG + cg], q3 = s_t[(r0 + 3) * PL_CG + cg];
+        uint32_t lo[4], hi[4];
+        transpose4x4_bytes(q0.x, q1.x, q2.x, q3.x, lo);
+        transpose4x4_bytes(q0.y, q1.y, q2.y, q3.y, hi);
         uint4* o = reinterpret_cast<uint4*>(out + (size_t)u * 8);
         o[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
         o[1] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
@@ -541,190 +505,178 @@ __global__ __launch_bounds__(256) void vt_qrec_kernel(const uint8_t* __restrict_
     for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
     if (lane == 0) s_red[wave] = part;
     __syncthreads();
-    for (int d = D::QS_OFF + threadIdx.x; d < D::REC_DW; d += blockDim.x)
-        out[d] = d == D::QS_OFF ? s_red[0] + s_red[1] + s_red[2] + s_red[3] : 0u;
+    if (threadIdx.x == 0) qsum[blockIdx.x] = s_red[0] + s_red[1] + s_red[2] + s_red[3];
 }
 
-// Start row SA(h) + I of one query against the template units it meets (3 or 4:
-// J - JLO(h) in [JA, JB], the same for both halves).  The borrow chains of those
-// units are interleaved plane by plane, so consecutive bitop3s are independent.
-// All indices are compile-time.
-template <int H, int I>
-__device__ __forceinline__ void plane_rows(const uint32_t (&P)[PlaneGeom<H>::NUH][8],
-                                           const uint32_t* sq, uint32_t (&acc)[2 * FAST_M - 1]) {
-    using G = PlaneGeom<H>;
-    constexpr int JA = I <= 2 ? 0 : (I + 1) / 4;
-    constexpr int JB0 = (I + 12) / 4;
-    constexpr int JB = JB0 < G::NUH - 1 ? JB0 : G::NUH - 1;
-    constexpr int NJ = JB - JA + 1;
-    static_assert(NJ >= 1 && NJ <= 4, "units per start row");
-    const uint4 lo = *reinterpret_cast<const uint4*>(sq + I * 8);
-    const uint4 hi = *reinterpret_cast<const uint4*>(sq + I * 8 + 4);
-    const uint32_t q[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+// Query start rows [M-3, H-M-1] are split into PL_SPLIT ranges, one wave each
+// per column group, so a wave keeps only the template units its rows meet
+// (10 of 16 at H = 64): fewer VGPRs, four waves per SIMD.
+constexpr int PL_SPLIT = 2;
+
+template <int H, int HALF>
+struct PlaneRange {
+    static constexpr int M = FAST_M, NU = H / 4, S0 = M - 3, S1 = H - M - 1, NS = S1 - S0 + 1;
+    static constexpr int NSH = (NS + PL_SPLIT - 1) / PL_SPLIT;
+    static constexpr int SA = S0 + HALF * NSH;
+    static constexpr int SB = (SA + NSH - 1) < S1 ? SA + NSH - 1 : S1;
+    static constexpr int ja(int s) { return (s - (M - 1)) > 0 ? (s - (M - 1) + 3) / 4 : 0; }
+    static constexpr int jb(int s) { return (s + (M - 1)) / 4 < NU - 1 ? (s + (M - 1)) / 4 : NU - 1; }
+    static constexpr int JLO = ja(SA), JHI = jb(SB), NUH = JHI - JLO + 1;
+};
+
+// One query start row S against the template units it meets (o = 4J - S within
+// +-(M-1): 3 or 4 units).  The borrow chains of those units are interleaved
+// plane by plane, so consecutive bitop3s are independent (a single chain would
+// stall on every instruction).  All indices are compile-time.
+template <int H, int HALF, int S>
+__device__ __forceinline__ void plane_row(const uint32_t (&P)[PlaneRange<H, HALF>::NUH][8],
+                                          const uint32_t* q, uint32_t (&acc)[2 * FAST_M - 1]) {
+    using R = PlaneRange<H, HALF>;
+    constexpr int M = FAST_M, JA = R::ja(S), JB = R::jb(S), NJ = JB - JA + 1;
+    static_assert(NJ >= 1 && NJ <= 4 && JA >= R::JLO && JB <= R::JHI, "units per query row");
     uint32_t b[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][0], q[0], 0u, 0x8E);
+    for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA - R::JLO + j][0], q[0], 0u, 0x8E);
 #pragma unroll
     for (int k = 1; k < 8; ++k)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) b[j] = __builtin_amdgcn_bitop3_b32(P[JA + j][k], q[k], b[j], 0x8E);
+        for (int j = 0; j < NJ; ++j)
+            b[j] = __builtin_amdgcn_bitop3_b32(P[JA - R::JLO + j][k], q[k], b[j], 0x8E);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        // offset index o + M - 1 = 4 (J - JLO) - I + 2 in both halves; v_bcnt's own
-        // accumulator (asm keeps the compiler from re-associating the counts into
-        // half-rate v_add3_u32)
-        uint32_t& a = acc[4 * (JA + j) - I + 2];
+        // v_bcnt's own accumulator (asm keeps the compiler from re-associating
+        // the counts into half-rate v_add3_u32)
+        uint32_t& a = acc[4 * (JA + j) - S + M - 1];
         asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(a) : "v"(b[j]), "v"(a));
     }
-    if constexpr (I + 1 < G::NSH) plane_rows<H, I + 1>(P, sq, acc);
+}
+
+// Query planes are staged per batch in LDS and read as wave-uniform
+// ds_read_b128 broadcasts into VGPRs: on gfx950 a VALU instruction with an SGPR
+// operand issues at about half the all-VGPR rate (tools/ubench_chain.hip:
+// 0.23 vs 0.36-0.41 wave-instructions per SIMD-cycle), so the chains take both
+// operands from VGPRs.
+template <int H, int HALF, int S>
+__device__ __forceinline__ void plane_rows(const uint32_t (&P)[PlaneRange<H, HALF>::NUH][8],
+                                           const uint32_t* sq, uint32_t (&acc)[2 * FAST_M - 1]) {
+    using R = PlaneRange<H, HALF>;
+    const uint4 lo = *reinterpret_cast<const uint4*>(sq + (S - R::S0) * 8);
+    const uint4 hi = *reinterpret_cast<const uint4*>(sq + (S - R::S0) * 8 + 4);
+    const uint32_t q[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    plane_row<H, HALF, S>(P, q, acc);
+    if constexpr (S < R::SB) plane_rows<H, HALF, S + 1>(P, sq, acc);
 }
 
 template <int H>
 struct PlaneLds {
-    uint32_t q[2][PlaneDims<H>::REC_DW];        // double-buffered query records (LDS-DMA)
-    unsigned long long key[PlaneDims<H>::WPB][256];  // per wave, per query of the chunk
+    static constexpr int M = FAST_M, NS = H - 2 * M + 3, NO = 2 * M - 1, NK = (NO + 1) / 2;
+    static constexpr int QW = PL_CG * NS * 8;                 // query-plane dwords per query
+    static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
+    uint4 q[PL_NB * QW / 4];                                   // the batch's query planes
+    uint32_t part[PL_NB][NK][NW][64];                          // u16 pairs: offsets 2k, 2k+1
+    uint32_t ts[16][64];                                       // TS(o) of the 64 templates
+    int batch;
 };
 
-constexpr int PL_QC_MAX = 256;   // queries per block (PlaneLds::key)
-
-// One LDS-DMA wave-instruction: 16 bytes per lane from gsrc to LDS byte address
-// lds + lane x 16.  Inline asm: hipcc would follow its builtin with an
-// s_waitcnt vmcnt(0) before the next LDS read of the other buffer (it cannot tell
-// the two apart), serialising the copy with the compute it is meant to hide
-// behind.  No VGPR is written, and the waits are explicit (plane scan loop).
-__device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\t"
-                 "s_mov_b32 m0, %2\n\t"
-                 "s_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds)
-                 : "memory");
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// Copy query record qi into LDS buffer dst: NCHUNK LDS-DMA wave-instructions of
-// 1 KiB, spread over the block's waves.  Completion: the issuing wave's
-// s_waitcnt vmcnt(0), then a barrier.
-template <int H>
-__device__ __forceinline__ void plane_stage(const uint32_t* __restrict__ rec, uint32_t* dst, int wave,
-                                            int lane) {
-    using D = PlaneDims<H>;
-#pragma unroll
-    for (int ch = 0; ch < D::NCHUNK; ch += D::WPB)
-        if (ch + wave < D::NCHUNK)
-            lds_dma16(rec + (ch + wave) * 256 + lane * 4,
-                      __builtin_amdgcn_readfirstlane(lds_addr(dst + (ch + wave) * 256)));
-}
-
-// Block b: template block tb = b / nqc, queries [c*qc, min(nq, (c+1)*qc)) with c = b % nqc.
-// With nqc a multiple of 8, blocks b and b + 8 (one XCD under round-robin dispatch;
-// speed only) take the same query chunks, so an XCD's L2 holds 1/8 of the queries.
-template <int H, bool MATRIX>
-__global__ __launch_bounds__(64 * PlaneDims<H>::WPB)
-__attribute__((amdgpu_waves_per_eu(PlaneGeom<H>::WAVES, PlaneGeom<H>::WAVES)))
-void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __restrict__ tsv,
-                          int64_t count, const uint32_t* __restrict__ qrec, int nq, int nqc,
-                          int qc, ScanOut out, int rank, int nranks) {
-    using D = PlaneDims<H>;
-    using G = PlaneGeom<H>;
-    __shared__ __attribute__((aligned(16))) PlaneLds<H> L;
-    const int tb = (int)(blockIdx.x / (unsigned)nqc), c = (int)(blockIdx.x % (unsigned)nqc);
-    const int q0 = c * qc, q1 = min(nq, q0 + qc);
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63, grp = lane / G::TPW, t = lane % G::TPW;
-    const int h = grp / PL_CG;
-    const int64_t slot = (int64_t)tb * 64 + wave * G::TPW + t;
-    if (q0 < q1) plane_stage<H>(qrec + (size_t)q0 * D::REC_DW, L.q[0], wave, lane);
-    uint32_t P[G::NUH][8];
+// The work of one wave: column group cg, query start rows of range HALF.
+template <int H, int HALF, bool MATRIX>
+__device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
+                                           int tb, int64_t count, const uint4* __restrict__ qp4,
+                                           const uint32_t* __restrict__ qsum, int nq,
+                                           unsigned* __restrict__ ctr, int G, int g, ScanOut out,
+                                           int rank, int nranks, int wave, int cg, int lane) {
+    using R = PlaneRange<H, HALF>;
+    using LD = PlaneLds<H>;
+    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
+    uint32_t P[R::NUH][8];
     {
-        const uint4* src = planes + ((size_t)tb * D::WPB + wave) * G::NUH * 128 + lane;
+        const uint4* src = planes + ((size_t)(tb * PL_CG + cg) * (H / 4) + R::JLO) * 128 + lane;
 #pragma unroll
-        for (int j = 0; j < G::NUH; ++j) {
+        for (int j = 0; j < R::NUH; ++j) {
             const uint4 a = src[(2 * j) * 64], b = src[(2 * j + 1) * 64];
             P[j][0] = a.x; P[j][1] = a.y; P[j][2] = a.z; P[j][3] = a.w;
             P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
         }
     }
-    uint32_t ts[G::KPL];
+    // this block's query group g of G: batches g, g + G, g + 2G, ...
+    const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
+    const int64_t slot = (int64_t)tb * 64 + lane;
+    const int tid = wave * 64 + lane;
+    for (;;) {
+        // two barriers per batch: (A) staged planes visible, (B) partial counts
+        // visible; the next batch is taken during the compute (L.batch is read
+        // before (A) and rewritten after it)
+        const int bi = L.batch;
+        if (bi >= nbatch) break;  // block-uniform
+        const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
+        for (int i = tid; i < nb * LD::QW / 4; i += NT) L.q[i] = qp4[(size_t)qb * (LD::QW / 4) + i];
+        __syncthreads();  // (A)
+        if (tid == 0) L.batch = (int)atomicAdd(ctr, 1u);
+#pragma unroll 1
+        for (int b = 0; b < nb; ++b) {
+            uint32_t acc[NO];
 #pragma unroll
-    for (int k = 0; k < G::KPL; ++k) ts[k] = tsv[(((size_t)tb * D::WPB + wave) * G::KPL + k) * 64 + lane];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's share of record q0
-    __syncthreads();
-    (void)h;
-    for (int qi = q0; qi < q1; ++qi) {
-        const int b = (qi - q0) & 1;
-        if (qi + 1 < q1) plane_stage<H>(qrec + (size_t)(qi + 1) * D::REC_DW, L.q[b ^ 1], wave, lane);
-        uint32_t acc[D::NO];
+            for (int o = 0; o < NO; ++o) acc[o] = 0u;
+            plane_rows<H, HALF, R::SA>(
+                P, reinterpret_cast<const uint32_t*>(L.q) + (b * PL_CG + cg) * NS * 8, acc);
 #pragma unroll
-        for (int o = 0; o < D::NO; ++o) acc[o] = 0u;
-        plane_rows<H, 0>(P, L.q[b] + grp * G::NSH * 8, acc);
-        const uint32_t qs = L.q[b][D::QS_OFF];
-        // counts per (template, offset) over the lane groups, packed u16 pairs (a
-        // lane's count <= 224, a template's <= (H-2M)*32 < 2^16): reduce-scatter, so
-        // lane group g ends with the totals of offsets [KPL*g, KPL*g + KPL)
-        uint32_t pk[8];
-#pragma unroll
-        for (int k = 0; k < 7; ++k) pk[k] = acc[2 * k] | (acc[2 * k + 1] << 16);
-        pk[7] = acc[14];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {    // lane bit 5: lower half keeps pk[k], upper pk[k + 4]
-            const auto r = __builtin_amdgcn_permlane32_swap(pk[k], pk[k + 4], false, false);
-            pk[k] = r[0] + r[1];
+            for (int k = 0; k < NK; ++k)
+                L.part[b][k][wave][lane] = acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u);
         }
+        __syncthreads();  // (B)
+        if (wave < nb) {  // wave w finishes query qb + w of the batch
+            const int qi = qb + wave;
+            uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {    // lane bit 4: even rows keep slot k, odd rows slot k + 2
-            const auto r = __builtin_amdgcn_permlane16_swap(pk[k], pk[k + 2], false, false);
-            pk[k] = r[0] + r[1];
-        }
-        uint32_t m;
-        if constexpr (D::NG == 8) {      // lane bit 3 (H = 64): offsets 2g, 2g + 1
-            const bool up = (lane >> 3) & 1;
-            const uint32_t keep = up ? pk[1] : pk[0], send = up ? pk[0] : pk[1];
-            const uint32_t tot = keep + __shfl_xor(send, 8);
-            m = min(ts[0] + 256u * (tot & 0xFFFFu), ts[1] + 256u * (tot >> 16));
-            const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-            m = min(r32[0], r32[1]);
-            const auto r16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-            m = min(r16[0], r16[1]);
-            m = min(m, (uint32_t)__shfl_xor(m, 8));
-        } else {                         // H = 32: offsets 4g .. 4g + 3
-            m = min(min(ts[0] + 256u * (pk[0] & 0xFFFFu), ts[1] + 256u * (pk[0] >> 16)),
-                    min(ts[2] + 256u * (pk[1] & 0xFFFFu), ts[3] + 256u * (pk[1] >> 16)));
-            const auto r32 = __builtin_amdgcn_permlane32_swap(m, m, false, false);
-            m = min(r32[0], r32[1]);
-            const auto r16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-            m = min(r16[0], r16[1]);
-        }
-        const uint32_t score = m - qs;
-        if constexpr (MATRIX) {
-            if (grp == 0 && slot < count) out.mat[(size_t)qi * out.ld + slot] = score;
-        } else {
-            const unsigned long long gidx = (unsigned long long)slot * nranks + rank;
-            unsigned long long key = slot < count ? (((unsigned long long)score << 32) | gidx) : NO_KEY;
+            for (int k = 0; k < NK; ++k) {
+                uint32_t t = 0;  // per-half sums stay < 2^16: no carry between the halves
 #pragma unroll
-            for (int off = 1; off < G::TPW; off <<= 1) {
-                const unsigned long long o = __shfl_xor(key, off);
-                key = o < key ? o : key;
+                for (int w = 0; w < LD::NW; ++w) t += L.part[wave][k][w][lane];
+                best = min(best, L.ts[2 * k][lane] + 256u * (t & 0xFFFFu));
+                if (2 * k + 1 < NO) best = min(best, L.ts[2 * k + 1][lane] + 256u * (t >> 16));
             }
-            if (lane == 0) L.key[wave][qi - q0] = key;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's share of record qi + 1
-        __syncthreads();   // buffer b free for the next DMA; the next record landed
-    }
-    if constexpr (!MATRIX) {
-        for (int k = threadIdx.x; k < q1 - q0; k += blockDim.x) {
-            unsigned long long m = L.key[0][k];
-#pragma unroll
-            for (int w = 1; w < D::WPB; ++w) m = L.key[w][k] < m ? L.key[w][k] : m;
-            atomicMin(out.best + q0 + k, m);
+            emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
         }
     }
+}
+
+// nqc blocks serve each template block; they take query batches of PL_NB from
+// the template block's counter, so blocks that the SIMDs' oldest-first issue
+// favours take more batches and no SIMD is left running a lone straggler.
+template <int H, bool MATRIX>
+__global__ __launch_bounds__(64 * PL_CG * PL_SPLIT) __attribute__((amdgpu_waves_per_eu(4, 4)))
+void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __restrict__ tsum,
+                          int ntb, int64_t count, const uint32_t* __restrict__ qp,
+                          const uint32_t* __restrict__ qsum, int nq, int nqc,
+                          unsigned* __restrict__ next_batch, ScanOut out, int rank, int nranks) {
+    static_assert(PL_SPLIT == 2, "two row ranges");
+    __shared__ PlaneLds<H> L;
+    // The nqc blocks of a template block are adjacent block ids, so they are dispatched
+    // together and split its query batches dynamically even when the grid runs in
+    // several rounds.  XCD-aware: blocks b and b+8 share an XCD (and its L2); with
+    // nqc >= 8 (a multiple of 8) the query batches are split into 8 groups by XCD, so
+    // each L2 holds one group's planes
+    const int tb = (int)(blockIdx.x / (unsigned)nqc);
+    const int G = nqc >= 8 ? 8 : 1, g = nqc >= 8 ? (int)(blockIdx.x & 7) : 0;
+    unsigned* ctr = next_batch + (size_t)tb * 8 + g;
+    VT_STAMP(0);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, cg = wave % PL_CG, half = wave / PL_CG;
+    for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
+    if (threadIdx.x == 0) L.batch = (int)atomicAdd(ctr, 1u);
+    __syncthreads();
+    const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
+    if (half == 0)
+        plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
+                                 wave, cg, lane);
+    else
+        plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
+                                 wave, cg, lane);
+    // Each of the nqc / G blocks sharing a counter ends on exactly one failed take, so
+    // the block whose take returned (group batches) + nqc / G - 1 is the counter's last
+    // user in this launch: it rewinds the counter for the next launch (no memset).
+    if (threadIdx.x == 0 && L.batch == ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G + nqc / G - 1) *ctr = 0u;
+    VT_STAMP(1);
 }
 
 // ===========================================================================
@@ -850,6 +802,7 @@ struct rs_vt {
     hipStream_t cstream = nullptr;           // rs_vt_match_stream's collective stream
     hipEvent_t evScan = nullptr, evComm = nullptr;
     uint32_t* dQpStream = nullptr;           // rs_vt_match_stream: every batch's query planes
+    uint32_t* dQsumStream = nullptr;
     size_t qpStreamCap = 0;                  // queries
     unsigned long long* dStream = nullptr;   // keys of rs_vt_match_stream, one row per batch
     unsigned long long* hStream = nullptr;   // pinned copy (nb * nq)
@@ -881,7 +834,10 @@ struct rs_vt {
     uint32_t* dCandP = nullptr;
     uint32_t* dCandTs = nullptr;
     uint32_t* dQp = nullptr;
+    uint32_t* dQsumRaw = nullptr;
     int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
+    unsigned* dCtr = nullptr;  // per template block x query group: next batch (plane scan)
+    int ctrCap = 0;
     // on-device subsampling of camera frames (rs_vt_set_subsample / rs_vt_match_frames)
     int32_t* dPix = nullptr;   // H*W byte offsets of the kept pixels in a frame
     int64_t frameBytes = 0;
@@ -893,16 +849,9 @@ struct rs_vt {
 namespace {
 
 size_t tblock_bytes(const rs_vt* h) { return (size_t)h->WD * h->HQ * 64 * 16; }
-// plane-scan buffers per 64-slot block and per query record (PlaneDims)
-size_t pblock_bytes(const rs_vt* h) {
-    return (size_t)(h->H == 64 ? PlaneDims<64>::PL_U4 : PlaneDims<32>::PL_U4) * 16;
-}
-size_t ts_block_bytes(const rs_vt* h) {
-    return (size_t)(h->H == 64 ? PlaneDims<64>::TS_DW : PlaneDims<32>::TS_DW) * 4;
-}
-size_t qrec_dwords(const rs_vt* h) {
-    return (size_t)(h->H == 64 ? PlaneDims<64>::REC_DW : PlaneDims<32>::REC_DW);
-}
+size_t pblock_bytes(const rs_vt* h) { return (size_t)PL_CG * (h->H / 4) * 128 * 16; }
+constexpr size_t TS_BLOCK_BYTES = 16 * 64 * sizeof(uint32_t);
+int plane_ns(const rs_vt* h) { return h->H - 2 * h->M + 3; }
 
 // (Re)allocate a slot buffer of `blocks` 64-slot blocks of `bb` bytes, keeping
 // the first `keep` blocks.
@@ -954,7 +903,7 @@ int vt_grow_lib(rs_vt* h, int64_t need_slots) {
     h->dLib = nl;
     if (h->planar) {
         RS_TRY(vt_realloc_blocks(h, (void**)&h->dLibP, h->localCap / 64, cap / 64, pblock_bytes(h)));
-        RS_TRY(vt_realloc_blocks(h, (void**)&h->dLibTs, h->localCap / 64, cap / 64, ts_block_bytes(h)));
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dLibTs, h->localCap / 64, cap / 64, TS_BLOCK_BYTES));
     }
     h->localCap = cap;
     return RS_OK;
@@ -971,10 +920,12 @@ int vt_grow_queries(rs_vt* h, int nq) {
     if (h->dBest) RS_HIP(hipFree(h->dBest));
     if (h->hBest) RS_HIP(hipHostFree(h->hBest));
     if (h->dQp) RS_HIP(hipFree(h->dQp));
-    h->dQp = nullptr;
+    if (h->dQsumRaw) RS_HIP(hipFree(h->dQsumRaw));
+    h->dQp = h->dQsumRaw = nullptr;
     const size_t qb = (size_t)h->H * h->W;
     if (h->planar) {
-        RS_HIP(hipMalloc(&h->dQp, sizeof(uint32_t) * qrec_dwords(h) * (size_t)cap));
+        RS_HIP(hipMalloc(&h->dQp, sizeof(uint32_t) * PL_CG * plane_ns(h) * 8 * (size_t)cap));
+        RS_HIP(hipMalloc(&h->dQsumRaw, sizeof(uint32_t) * cap));
     }
     RS_HIP(hipMalloc(&h->dQraw, qb * cap));
     RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocDefault));
@@ -1024,7 +975,7 @@ int vt_grow_cand(rs_vt* h, int64_t slots) {
     RS_HIP(hipMalloc(&h->dCand, (size_t)(cap / 64) * tblock_bytes(h)));
     if (h->planar) {
         RS_TRY(vt_realloc_blocks(h, (void**)&h->dCandP, 0, cap / 64, pblock_bytes(h)));
-        RS_TRY(vt_realloc_blocks(h, (void**)&h->dCandTs, 0, cap / 64, ts_block_bytes(h)));
+        RS_TRY(vt_realloc_blocks(h, (void**)&h->dCandTs, 0, cap / 64, TS_BLOCK_BYTES));
     }
     h->candCap = cap;
     return RS_OK;
@@ -1047,10 +998,9 @@ int vt_build_forms(rs_vt* h, int nq, const uint8_t* src) {
     if (!h->planar)
         hipLaunchKernelGGL(vt_qform_kernel, dim3(nq), dim3(256), 0, h->stream, src, h->H, h->W,
                            h->WD, h->M, h->dQf, h->dQsum);
-    else if (h->H == 64)
-        hipLaunchKernelGGL(vt_qrec_kernel<64>, dim3(nq), dim3(256), 0, h->stream, src, h->dQp);
     else
-        hipLaunchKernelGGL(vt_qrec_kernel<32>, dim3(nq), dim3(256), 0, h->stream, src, h->dQp);
+        hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, src, h->H,
+                           h->M, h->dQp, h->dQsumRaw);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
@@ -1102,70 +1052,64 @@ int vt_store(rs_vt* h, bool cand, const uint8_t* d_raw, int n) {
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(vt_store_kernel, dim3(grid), dim3(256), 0, h->stream, d_raw, h->dSrc,
                        h->dDst, n, lib, h->H, h->W, h->WD, h->HQ);
-    if (h->planar) {
-        uint4* planes = reinterpret_cast<uint4*>(cand ? h->dCandP : h->dLibP);
-        uint32_t* ts = cand ? h->dCandTs : h->dLibTs;
-        if (h->H == 64)
-            hipLaunchKernelGGL(vt_plane_store_kernel<64>, dim3(n), dim3(256), 0, h->stream, d_raw,
-                               h->dSrc, h->dDst, planes, ts);
-        else
-            hipLaunchKernelGGL(vt_plane_store_kernel<32>, dim3(n), dim3(256), 0, h->stream, d_raw,
-                               h->dSrc, h->dDst, planes, ts);
-    }
+    if (h->planar)
+        hipLaunchKernelGGL(vt_plane_store_kernel, dim3(n), dim3(256), 0, h->stream, d_raw, h->dSrc,
+                           h->dDst, h->H, h->M, cand ? h->dCandP : h->dLibP,
+                           cand ? h->dCandTs : h->dLibTs);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
 
-// Query chunks per template block (nqc) and queries per chunk (qc) of the plane
-// scan.  A block's fixed cost -- its template planes into VGPRs, about the work
-// of a few queries -- favours long chunks; the last round of resident blocks
-// favours a grid that fills whole rounds.  Cost model: rounds x (qc + 4).
-// nqc is a multiple of 8 where the batch allows (the XCD query groups).
-// RS_VT_NQC overrides (A/B, tests).
-void plane_chunks(int ntb, int nq, int slots, int* nqc_out, int* qc_out) {
-    int best_nqc = 1;
+// Blocks per template block (nqc) for the plane scan.  A block's fixed cost
+// (its template planes, 128 KiB, into VGPRs) is small next to its query batches,
+// and the nqc blocks of a template block balance their batches dynamically, so
+// finer splits fill the last round of resident blocks better; measured on
+// MI355X (tools/scan_split.py, 1,024 queries): nqc = 32 is within 2% of the best
+// split from 12.5k to 100k templates (100k: 18.6 ms at nqc = 1, the previous
+// choice there, vs 15.0 ms), and small libraries gain from up to 4 rounds of
+// blocks (1k: 128 -> 0.183 ms vs 0.199 ms at 32).  nqc >= 8 is a multiple of 8
+// (the XCD query groups).  RS_VT_NQC overrides (A/B).
+int plane_split(int ntb, int nbatch, int slots) {
+    int nqc;
     if (const char* e = std::getenv("RS_VT_NQC")) {
-        best_nqc = std::max(1, std::min(std::atoi(e), nq));
+        nqc = std::max(1, std::atoi(e));
     } else {
-        double best = 1e300;
-        const int lo = (nq + PL_QC_MAX - 1) / PL_QC_MAX;
-        for (int nqc = lo; nqc <= std::min(nq, 4096); ++nqc) {
-            if (nq >= 64 && nqc % 8 != 0) continue;
-            const int qc = (nq + nqc - 1) / nqc;
-            const int used = (nq + qc - 1) / qc;
-            const double rounds = std::ceil((double)ntb * used / std::max(1, slots));
-            const double cost = rounds * (qc + 4);
-            if (cost < best - 1e-9) {
-                best = cost;
-                best_nqc = nqc;
-            }
-        }
+        const int fill = (slots + ntb - 1) / ntb;  // blocks per template block for one round
+        nqc = std::max(32, std::min(4 * fill, std::max(128, fill)));
     }
-    int qc = (nq + best_nqc - 1) / best_nqc;
-    qc = std::max(qc, (nq + PL_QC_MAX - 1) / PL_QC_MAX);
-    if (qc > PL_QC_MAX) qc = PL_QC_MAX;
-    *qc_out = qc;
-    *nqc_out = (nq + qc - 1) / qc;
+    nqc = std::min(nqc, std::max(1, nbatch));
+    if (nqc >= 8) nqc &= ~7;
+    return nqc;
 }
 
+// Launch a scan of queries [0, nq) (forms in dQf) against `count` slots of lib.
 template <bool MATRIX>
 int vt_launch_plane(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int rank,
                     int nranks, int64_t tb0) {
     const int ntb = (int)((count + 63) / 64);
-    int nqc = 1, qc = 1;
-    plane_chunks(ntb, nq, h->planeSlots, &nqc, &qc);
+    const int nqc = plane_split(ntb, (nq + PL_NB - 1) / PL_NB, h->planeSlots);
+    if (8 * ntb > h->ctrCap) {  // counters start at zero and every scan leaves them at zero
+        const int cap = std::max(8 * ntb, 2 * h->ctrCap);
+        if (h->dCtr) RS_HIP(hipFree(h->dCtr));
+        h->dCtr = nullptr;
+        h->ctrCap = 0;
+        RS_HIP(hipMalloc(&h->dCtr, sizeof(unsigned) * (size_t)cap));
+        RS_HIP(hipMemsetAsync(h->dCtr, 0, sizeof(unsigned) * (size_t)cap, h->stream));
+        h->ctrCap = cap;
+    }
     RS_CHECK((int64_t)ntb * nqc < (1ll << 31), RS_ERR_ARG, "scan grid too large");
     const dim3 grid((unsigned)(ntb * nqc));
     const uint4* planes = reinterpret_cast<const uint4*>(
         reinterpret_cast<const uint8_t*>(cand ? h->dCandP : h->dLibP) + (size_t)tb0 * pblock_bytes(h));
-    const uint32_t* ts = reinterpret_cast<const uint32_t*>(
-        reinterpret_cast<const uint8_t*>(cand ? h->dCandTs : h->dLibTs) + (size_t)tb0 * ts_block_bytes(h));
+    const uint32_t* ts = (cand ? h->dCandTs : h->dLibTs) + (size_t)tb0 * (TS_BLOCK_BYTES / 4);
     if (h->H == 64)
-        hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PlaneDims<64>::WPB), 0,
-                           h->stream, planes, ts, count, h->dQp, nq, nqc, qc, out, rank, nranks);
+        hipLaunchKernelGGL((vt_scan_plane_kernel<64, MATRIX>), grid, dim3(64 * PL_CG * PL_SPLIT), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, h->dCtr, out, rank,
+                           nranks);
     else
-        hipLaunchKernelGGL((vt_scan_plane_kernel<32, MATRIX>), grid, dim3(64 * PlaneDims<32>::WPB), 0,
-                           h->stream, planes, ts, count, h->dQp, nq, nqc, qc, out, rank, nranks);
+        hipLaunchKernelGGL((vt_scan_plane_kernel<32, MATRIX>), grid, dim3(64 * PL_CG * PL_SPLIT), 0, h->stream,
+                           planes, ts, ntb, count, h->dQp, h->dQsumRaw, nq, nqc, h->dCtr, out, rank,
+                           nranks);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
@@ -1393,40 +1337,51 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     h->timedScan = false;
     const int64_t lc = local_count_of(h, h->count);
     // Device-resident batches of the plane scan: one launch builds every batch's
-    // planes (nb * nq blocks), then the scans run back to back, each pointed at
-    // its batch's slice.
+    // planes (nb * nq blocks) and ONE scan launch covers all nb * nq queries (the
+    // batches are independent against a frozen library, and their keys are rows of
+    // one array), so the scan's fixed costs -- each block's template planes into
+    // VGPRs, the last partial round of blocks -- are paid once per call instead of
+    // once per batch; a sharded handle then min-reduces all rows in one collective.
     const bool allplanes = on_device && h->planar && nb > 1;
-    const size_t qpq = h->planar ? qrec_dwords(h) : 0;  // record dwords per query
-    struct PlaneBufRestore {  // h->dQp points at the per-batch buffers on return
+    const size_t qpq = (size_t)PL_CG * plane_ns(h) * 8;  // plane dwords per query
+    struct PlaneBufRestore {  // h->dQp / dQsumRaw point at the per-batch buffers on return
         rs_vt* h;
         uint32_t* p;
-        ~PlaneBufRestore() { h->dQp = p; }
-    } restore{h, h->dQp};
+        uint32_t* q;
+        ~PlaneBufRestore() { h->dQp = p; h->dQsumRaw = q; }
+    } restore{h, h->dQp, h->dQsumRaw};
     if (allplanes) {
         if (total > h->qpStreamCap) {
             if (h->dQpStream) RS_HIP(hipFree(h->dQpStream));
-            h->dQpStream = nullptr;
+            if (h->dQsumStream) RS_HIP(hipFree(h->dQsumStream));
+            h->dQpStream = h->dQsumStream = nullptr;
             h->qpStreamCap = 0;
             RS_HIP(hipMalloc(&h->dQpStream, sizeof(uint32_t) * qpq * total));
+            RS_HIP(hipMalloc(&h->dQsumStream, sizeof(uint32_t) * total));
             h->qpStreamCap = total;
         }
         RS_CHECK(total <= INT32_MAX, RS_ERR_ARG, "too many queries in one stream");
         h->dQp = h->dQpStream;
+        h->dQsumRaw = h->dQsumStream;
         RS_TRY(vt_build_forms(h, (int)total, queries));
+        const ScanOut out{h->dStream, nullptr, 0};
+        RS_TRY(vt_launch_scan<false>(h, false, lc, (int)total, out, h->rank, h->nranks));
+        if (h->comm) {
+            ncclResult_t r = ncclAllReduce(h->dStream, h->dStream, total, ncclUint64, ncclMin, h->comm,
+                                           h->stream);
+            RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
+                     ncclGetErrorString(r));
+        }
     }
-    for (int b = 0; b < nb; ++b) {
+    for (int b = 0; b < nb && !allplanes; ++b) {
         unsigned long long* keys = h->dStream + (size_t)b * nq;
         const ScanOut out{keys, nullptr, 0};
         const uint8_t* src = queries + qb * b;
-        if (allplanes) {
-            h->dQp = h->dQpStream + qpq * nq * b;  // launch arguments are captured at enqueue
-        } else {
-            if (!on_device) {
-                RS_HIP(hipMemcpyAsync(h->dQraw, src, qb, hipMemcpyHostToDevice, h->stream));
-                src = h->dQraw;
-            }
-            RS_TRY(vt_build_forms(h, nq, src));
+        if (!on_device) {
+            RS_HIP(hipMemcpyAsync(h->dQraw, src, qb, hipMemcpyHostToDevice, h->stream));
+            src = h->dQraw;
         }
+        RS_TRY(vt_build_forms(h, nq, src));
         RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
         if (h->comm) {
             // the batch's row is reduced on the collective stream while the next
@@ -1439,7 +1394,7 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
                      ncclGetErrorString(r));
         }
     }
-    if (h->comm) {
+    if (h->comm && !allplanes) {
         RS_HIP(hipEventRecord(h->evComm, h->cstream));
         RS_HIP(hipStreamWaitEvent(h->stream, h->evComm, 0));
     }
@@ -1503,8 +1458,7 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
         hipFuncAttributes fa{};
         const void* fn = h->H == 64 ? reinterpret_cast<const void*>(vt_scan_plane_kernel<64, false>)
                                     : reinterpret_cast<const void*>(vt_scan_plane_kernel<32, false>);
-        const int wpb = h->H == 64 ? PlaneDims<64>::WPB : PlaneDims<32>::WPB;
-        hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * wpb, 0);
+        hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * PL_CG * PL_SPLIT, 0);
         if (oe == hipSuccess) oe = hipFuncGetAttributes(&fa, fn);
         if (oe == hipSuccess) oe = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (oe != hipSuccess) {
@@ -1513,7 +1467,7 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
             return RS_ERR_HIP;
         }
         const int vg = std::max(8, (fa.numRegs + 7) / 8 * 8);
-        const int by_vgpr = (512 / vg) * 4 / wpb;  // waves/SIMD x 4 SIMDs / waves/block
+        const int by_vgpr = (512 / vg) * 4 / (PL_CG * PL_SPLIT);  // waves/SIMD x 4 SIMDs / waves/block
         const int by_lds = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) : per_cu;
         const int api = per_cu;
         per_cu = std::max(1, std::min({api, by_vgpr, by_lds}));
@@ -1550,11 +1504,12 @@ int rs_vt_destroy(rs_vt* h) {
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
                     (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
-                    (void*)h->dPix, (void*)h->dFrames})
+                    (void*)h->dQsumRaw, (void*)h->dCtr, (void*)h->dPix, (void*)h->dFrames})
         if (p) (void)hipFree(p);
     if (h->hStream) (void)hipHostFree(h->hStream);
     if (h->dStream) (void)hipFree(h->dStream);
     if (h->dQpStream) (void)hipFree(h->dQpStream);
+    if (h->dQsumStream) (void)hipFree(h->dQsumStream);
     for (void* p : {(void*)h->hQraw, (void*)h->hBest, (void*)h->hSrc, (void*)h->hDst, (void*)h->hMat,
                     (void*)h->hFrames})
         if (p) (void)hipHostFree(p);

@@ -473,3 +473,25 @@ def test_match_stream_collective_path_one_rank(vtmod):
         assert np.array_equal(idx[b], i) and np.array_equal(score[b], sc)
     s.close()
     plain.close()
+
+
+def test_match_stream_device_batches_collective_one_rank(vtmod):
+    """HBM-resident batches through a 1-rank RCCL communicator: one fused scan of all
+    batches, one collective over every row; equal to the per-batch frozen matching."""
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(900, 64, 32, seed=19)
+    batches = np.stack([V.synthetic_queries(lib_np, 200, seed=60 + b)[0] for b in range(5)])
+    uid = vtmod.ShardedViewTemplates.unique_id()
+    s = vtmod.ShardedViewTemplates.from_shape((64, 32), 45000, 0, 1, reducer='rccl', unique_id=uid)
+    plain = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    s.add(lib_np)
+    plain.add(lib_np)
+    buf = _lib.DeviceBuffer(batches.nbytes).upload(batches)
+    for _ in range(2):
+        idx, score = s.match_stream((5, 200, buf))
+        for b in range(5):
+            i, sc, _ = plain.match_templates(batches[b], mode=0)
+            assert np.array_equal(idx[b], i) and np.array_equal(score[b], sc)
+    buf.close()
+    s.close()
+    plain.close()
