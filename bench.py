@@ -166,6 +166,7 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
             qs.append(q_)
             srcs.append(s_)
         bufs = _lib.DeviceBuffer(Q * queries[0].nbytes * nres, device=d.dev).upload(np.stack(qs))
+        first_step = np.ascontiguousarray(np.concatenate(qs[:min(bps, nres)]))
         del qs
         nchunk = max(1, nres // bps)
         bpc = min(bps, nres)
@@ -211,12 +212,22 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
                 s_ = srcs[c * bpc + b]
                 correct = correct and bool(np.all(sidx[b][s_ >= 0] == s_[s_ >= 0]))
         bufs.close()
-        match(staged=False)                  # re-stage one batch for the timed-scan pass
     vts.set_timing(True)
+    # the scan kernel's duration as the timed steps launch it: the stream scans all
+    # of a step's HBM-resident batches (bpc x Q queries) in one launch
     kernel_ms = []
-    for _ in range(max(10, min(steps * bpc, 100))):
-        match(staged=True)
-        kernel_ms.append(vts.device_ms())
+    if pipeline == 'stream':
+        big = first_step
+        _lib.check(lib.rs_vt_match_batch(vts._h, len(big), _lib.ptr(big, ctypes.c_uint8),
+                                         _lib.RS_VT_FROZEN, None, None, None))
+        for _ in range(max(5, min(steps, 30))):
+            _lib.check(lib.rs_vt_match_batch(vts._h, len(big), None, _lib.RS_VT_FROZEN, None, None, None))
+            kernel_ms.append(vts.device_ms())
+        match(staged=False)                  # stage one batch again for the PCIe-inclusive rate
+    else:
+        for _ in range(max(10, min(steps, 100))):
+            match(staged=True)
+            kernel_ms.append(vts.device_ms())
     # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
     d.barrier()
     p0 = time.perf_counter()
@@ -237,7 +248,8 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
         'scan_ms': float(np.mean(kernel_ms)),
         'scan_ms_min': float(np.min(kernel_ms)),
         'kernel': SCAN_KERNELS.get(vts.scan_form(), vts.scan_form()),
-        'compares_per_launch': float(len(range(d.rank, total, n))) * Q,
+        'compares_per_launch': float(len(range(d.rank, total, n))) * Q * bpc,
+        'queries_per_launch': Q * bpc,
         'templates_per_launch': len(range(d.rank, total, n)),
         'reduce': reduce_kind,
         'pipeline': pipeline,
@@ -262,7 +274,8 @@ def scan_roofline(tv, tj, key):
     configuration (templates per launch, queries), from profiles/."""
     rec = (tj.get('scans') or {}).get(key) or {}
     same = (rec.get('templates_per_launch') == tv['templates_per_launch']
-            and rec.get('queries') is not None and rec.get('kernel', '').startswith(tv['kernel']))
+            and rec.get('queries') == tv['queries_per_launch']
+            and rec.get('kernel', '').startswith(tv['kernel']))
     scan_s = tv['scan_ms'] * 1e-3
     roof = {'bound': 'valu', 'unit': 'G wave-instructions/s', 'peak': VALU_PEAK_GINSTS,
             'achieved': None, 'frac': None, 'traffic': None,
@@ -279,8 +292,7 @@ def scan_roofline(tv, tj, key):
             roof['hbm_frac'] = roof['hbm_achieved_GBs'] / HBM_PEAK_GBS
     # unique bytes a launch must move: the stored templates (bytes + planes + sums)
     # once, the queries' planes once
-    uniq = tv['templates_per_launch'] * (2048 + 4096 + 64) + tv['compares_per_launch'] / max(
-        1, tv['templates_per_launch']) * (4 * 51 * 32 + 4)
+    uniq = tv['templates_per_launch'] * (2048 + 4096 + 64) + tv['queries_per_launch'] * (4 * 51 * 32 + 4)
     roof['unique_bytes_per_launch'] = uniq
     if roof['traffic']:
         roof['traffic_over_unique'] = roof['traffic'] / uniq

@@ -23,7 +23,7 @@ import json
 import os
 import re
 
-SCANS = {'headline': 1000, 'stress': 10000, 'library': 100000}
+SCANS = {'headline': (1000, 10240), 'stress': (10000, 5120), 'library': (100000, 2048)}
 PCS = {'pc64': ('rows', [64, 64, 36]), 'pc128': ('stream', [128, 128, 72])}
 
 
@@ -91,7 +91,6 @@ def main():
     ap.add_argument('--dir', required=True)
     ap.add_argument('--tag', required=True)
     ap.add_argument('--out', default='profiles')
-    ap.add_argument('--queries', type=int, default=1024)
     a = ap.parse_args()
     summary = {'tag': a.tag, 'method': __doc__.strip().splitlines()[2:11], 'configs': {}}
     traffic = {'source': f'{a.tag}_pmc_summary.json', 'scans': {}, 'pose_cell': {}}
@@ -107,7 +106,7 @@ def main():
             k = max(scan, key=lambda n: ks[n]['trace']['calls'])
             e = ks[k]
             traffic['scans'][{'headline': 'headline', 'stress': 'stress', 'library': 'library'}[c]] = {
-                'kernel': k, 'templates_per_launch': SCANS[c], 'queries': a.queries,
+                'kernel': k, 'templates_per_launch': SCANS[c][0], 'queries': SCANS[c][1],
                 'kernel_us_rocprof': e['trace']['avg_us'],
                 'valu_insts_per_launch': e.get('sq', {}).get('SQ_INSTS_VALU'),
                 'hbm_bytes_per_launch': e.get('hbm_bytes_per_dispatch'),
