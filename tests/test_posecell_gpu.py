@@ -190,12 +190,12 @@ def test_simulate_driver(pcn):
 
 
 # every step-kernel form (RS_PC_FORM) against the oracle: the row-tiled and 3-D
-# tiled single-pass forms, the four-pass form and the layer-streaming form at several tile shapes
+# tiled single-pass forms and the layer-streaming form at several tile shapes
 # (rows per wave, row groups, layers per block), incl. ragged tiles and grids
 # whose theta extent is not a multiple of the chunk
-FORMS = {'float32': ['rows', 'passes', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
+FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
                      'stream:1,4,2,3', 'stream:2,4,2,6'],
-         'float64': ['rows', 'passes', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
+         'float64': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
@@ -216,6 +216,31 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
             assert [tuple(m) for m in got] == maxes, (shape, form)
             assert np.abs(net.posecells - want).max() < tol, (shape, form)
             net.close()
+
+
+@pytest.mark.parametrize('shape', [(64, 64, 36), (16, 64, 10), (40, 64, 13), (100, 64, 9), (7, 64, 7)])
+def test_persistent_form_agrees_with_oracle(pcn, monkeypatch, shape):
+    """RS_PC_FORM=persist: a batch of steps in one launch on one XCD (two in-launch
+    barriers per step); grids with fewer x rows than blocks, ragged row bands and
+    theta chunks; a single update() on the same handle takes the rows kernels."""
+    monkeypatch.setenv('RS_PC_FORM', 'persist')
+    od = odometry(12, 23)
+    loc = tuple(s // 2 for s in shape)
+    ref = P.PoseCellOracle(shape)
+    ref.inject(1, loc)
+    maxes = [ref.update(v) for v in od]
+    net = pcn(shape)
+    assert net.step_form() == 'persist'
+    net.inject(1, loc)
+    got = net.run(od[:11])
+    assert [tuple(m) for m in got] == maxes[:11], shape
+    assert net.update(od[11]) == maxes[11]
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL, shape
+    got = net.run(od[:0])
+    assert got.shape == (0, 3)
+    net.close()
+    with pytest.raises(ValueError):
+        pcn(shape, precision='float64')
 
 
 def test_default_form_by_grid_size(pcn, monkeypatch):

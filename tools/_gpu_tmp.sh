@@ -1,5 +1,5 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-for t in 1000 10000; do
-timeout -k 10 300 python tools/scan_ab.py tools/ab/old.so tools/ab/nh2.so tools/ab/nh1.so --templates $t --reps 20 || exit $?
-done
-timeout -k 10 300 python tools/scan_ab.py tools/ab/old.so tools/ab/nh1.so --templates 100000 --reps 3 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_posecell_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "persistent" > gpurun_out/pc_persist.log 2>&1; rc=$?
+tail -3 gpurun_out/pc_persist.log
+case $rc in 124|134|137|139) exit $rc;; esac
+timeout -k 10 200 python tools/pc_sweep.py --shape 64,64,36 --steps 2000 --check-steps 20 --forms rows persist:1 persist:2 persist:4 persist:8 rows persist:2 2>&1 | grep "{"
