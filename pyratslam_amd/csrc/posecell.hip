@@ -1071,277 +1071,6 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     PC_STAMP(3, 4);
 }
 
-// ---------------------------------------------------------------------------
-// Persistent form (RS_PC_FORM=persist; float32, Y == 64): a whole batch of
-// update() steps in ONE launch on the compute units of one XCD, which share an
-// L2.  Each participating block owns a band of x rows; per step
-//   excite (x, y, theta passes, inhibition, partial sum) -> XCD barrier ->
-//   path (shifted 7x7, clamp, theta pass, clamp, / total, argmax) -> XCD barrier,
-// so a step costs two in-launch barriers instead of two kernel boundaries, and
-// the volumes stay in that XCD's L2.  Lane = y column (Y = 64 = the wave), so
-// the y taps are DPP wave rotations (the wrap in y is the wave's own rotation);
-// the x taps are loads of the neighbouring rows; theta runs on a 7-deep
-// register ring per wave over a chunk of layers (+6 halo layers).
-// Hand-off between blocks (MI355X_MICROARCH.md, Valid forms, row 3): every byte
-// another block reads is stored and loaded with sc1 (L2, whole 256-byte rows per
-// wave instruction), each block signals with one agent-scope atomic add after
-// its waves' vmcnt(0) and a workgroup barrier, and the waiting block polls with
-// sc1 loads and then joins a workgroup barrier.
-// Participants: the blocks the dispatcher places on XCC 0 (counted at launch:
-// every block registers, the others exit), so the protocol needs no assumption
-// about placement; the host checks that some block participated.
-// ---------------------------------------------------------------------------
-constexpr int PS_NT = 512;                  // 8 waves per block
-constexpr int PS_NL = 11;                   // input layers per unit (chunk of <= 5 + 6 halo), all loaded at once
-constexpr unsigned PS_SPIN_LIMIT = 1u << 22;   // ~0.1 s per wait, then give up (flagged)
-
-struct PsSync {              // zeroed before every launch
-    unsigned arrive;         // blocks that have registered
-    unsigned count;          // participants (blocks on XCC 0)
-    unsigned bar;            // monotonic XCD barrier counter
-    unsigned timeout;        // set if a spin gave up (results invalid)
-};
-
-__device__ __forceinline__ float ld_sc1(const float* p) {
-    return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// value of lane (lane + d) mod 64, d in [-3, 3] (DPP wave rotations by one lane)
-__device__ __forceinline__ float wave_rot(float v, int d) {
-    int x = __float_as_int(v);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        if (i < d) x = __builtin_amdgcn_update_dpp(0, x, 0x134, 0xF, 0xF, false);   // wave_rol:1
-        if (i < -d) x = __builtin_amdgcn_update_dpp(0, x, 0x13C, 0xF, 0xF, false);  // wave_ror:1
-    }
-    return __int_as_float(x);
-}
-
-__device__ void ps_barrier(PsSync* s, unsigned target) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 stores reached L2
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(&s->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
-        while (__hip_atomic_load(&s->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-               __hip_atomic_load(&s->timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins == PS_SPIN_LIMIT) {
-                __hip_atomic_store(&s->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(PS_NT) void pc_persist_kernel(float* __restrict__ P, float* __restrict__ Q,
-                                                            double* __restrict__ part,
-                                                            const unsigned char* __restrict__ ctl,
-                                                            size_t ctl_stride, size_t off_oy, size_t off_f,
-                                                            size_t off_zf, const float* __restrict__ filt,
-                                                            SepKernel<float> k,
-                                                            unsigned long long* __restrict__ res, int n,
-                                                            int X, int TH, int nxcd,
-                                                            PsSync* __restrict__ sync) {
-    constexpr int Y = 64;
-    __shared__ int s_rank, s_np;
-    __shared__ float s_bv[PS_NT / 64];
-    __shared__ unsigned s_bl[PS_NT / 64];
-    __shared__ double s_red[PS_NT / 64];
-    if (threadIdx.x == 0) {
-        unsigned xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        int r = -1;
-        if ((int)(xcc & 7) < nxcd)
-            r = (int)__hip_atomic_fetch_add(&sync->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the count add has returned before this block arrives
-        __hip_atomic_fetch_add(&sync->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        int np = 0;
-        if (r >= 0) {
-            unsigned spins = 0;
-            while (__hip_atomic_load(&sync->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins == PS_SPIN_LIMIT) {
-                    __hip_atomic_store(&sync->timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    r = -1;
-                    break;
-                }
-            }
-            np = (int)__hip_atomic_load(&sync->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_rank = r;
-        s_np = np;
-    }
-    __syncthreads();
-    const int rank = s_rank, np = s_np;
-    if (rank < 0) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // units (x row, theta chunk of CH layers) over every participating wave
-    const int nwaves = np * (PS_NT / 64), gw = rank * (PS_NT / 64) + wave;
-    int nch = max(1, nwaves / X);
-    while ((TH + nch - 1) / nch + 2 * HALF > PS_NL) ++nch;   // a unit's layers fit the load batch
-    const int CH = (TH + nch - 1) / nch;
-    const int nunits = X * nch;
-    const size_t LS = (size_t)X * Y;   // layer stride
-    unsigned target = 0;
-    for (int s = 0; s < n; ++s) {
-        const unsigned char* rec = ctl + (size_t)s * ctl_stride;
-        const int* cox = reinterpret_cast<const int*>(rec);
-        const int* coy = reinterpret_cast<const int*>(rec + off_oy);
-        const int* cfi = reinterpret_cast<const int*>(rec + off_f);
-        const double* czf = reinterpret_cast<const double*>(rec + off_zf);
-        // ---- excitation (posecell_network.py:336-343): x, y, theta passes -----------
-        double sum = 0.0;
-        for (int u = gw; u < nunits; u += nwaves) {
-            const int i = u % X, c = u / X;
-            const int o0 = c * CH, o1 = min(TH, o0 + CH);
-            if (o0 >= o1) continue;
-            int rows[FL];
-#pragma unroll
-            for (int t = 0; t < FL; ++t) rows[t] = rs::wrapi(i - HALF + t, X) * Y + lane;
-            // every input layer of the unit (o0-3 .. o1+2) loaded at once: one L2 round
-            // trip per unit; then x, y passes per layer and theta on a 7-slot ring
-            const int nL = o1 - o0 + 2 * HALF;
-            float in[PS_NL][FL];
-#pragma unroll
-            for (int it = 0; it < PS_NL; ++it)
-                if (it < nL) {
-                    const float* src = P + (size_t)rs::wrapi(o0 - HALF + it, TH) * LS;
-#pragma unroll
-                    for (int t = 0; t < FL; ++t) in[it][t] = ld_sc1(src + rows[t]);
-                }
-            float re[FL], ri[FL];
-#pragma unroll
-            for (int it = 0; it < PS_NL; ++it) {
-                if (it >= nL) continue;   // (constant trip count: the arrays stay in registers)
-                float xe = 0.f, xi = 0.f;
-#pragma unroll
-                for (int t = 0; t < FL; ++t) {
-                    xe += k.ge[t] * in[it][t];
-                    xi += k.gi[t] * in[it][t];
-                }
-                float ye = 0.f, yi = 0.f;
-#pragma unroll
-                for (int t = 0; t < FL; ++t) {
-                    ye += k.ge[t] * wave_rot(xe, t - HALF);
-                    yi += k.gi[t] * wave_rot(xi, t - HALF);
-                }
-                re[it % FL] = ye;
-                ri[it % FL] = yi;
-                if (it >= 2 * HALF) {
-                    const int o = o0 + it - 2 * HALF;
-                    float e = 0.f, g = 0.f;
-#pragma unroll
-                    for (int t = 0; t < FL; ++t) {   // input layer o - 3 + t sits in slot (it + 1 + t) % 7
-                        e += k.ge[t] * re[(it + 1 + t) % FL];
-                        g += k.gi[t] * ri[(it + 1 + t) % FL];
-                    }
-                    const float v = (e - g) * k.scale;
-                    const float q = v < k.inhib ? 0.f : v - k.inhib;
-                    st_sc1(Q + (size_t)o * LS + (size_t)i * Y + lane, q);
-                    sum += (double)q;
-                }
-            }
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
-        if (lane == 0) s_red[wave] = sum;
-        __syncthreads();
-        if (tid == 0) {
-            double t = 0.0;
-            for (int w = 0; w < PS_NT / 64; ++w) t += s_red[w];
-            __hip_atomic_store(part + rank, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        target += np;
-        ps_barrier(sync, target);
-        // ---- path integration (posecell_network.py:252-314) + normalisation + argmax ---
-        // normalisation total: the blocks' partials, one per lane, summed in a fixed order
-        double tot = 0.0;
-        for (int b = lane; b < np; b += 64) tot += __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off);
-        const float tt = (float)tot;
-        float zf[FL];
-#pragma unroll
-        for (int z = 0; z < FL; ++z) zf[z] = (float)czf[z];
-        float bv = -1.f;
-        unsigned bl = 0xFFFFFFFFu;
-        for (int u = gw; u < nunits; u += nwaves) {
-            const int i = u % X, c = u / X;
-            const int o0 = c * CH, o1 = min(TH, o0 + CH);
-            if (o0 >= o1) continue;
-            // every shifted window row of the unit's layers loaded at once
-            const int nL = o1 - o0 + 2 * HALF;
-            float w[PS_NL][FL];
-#pragma unroll
-            for (int it = 0; it < PS_NL; ++it)
-                if (it < nL) {
-                    const int L = rs::wrapi(o0 - HALF + it, TH);
-                    const int ox = rs::wrapi(cox[L], X), oy = rs::wrapi(coy[L], Y);
-                    const float* src = Q + (size_t)L * LS + ((lane + oy) & (Y - 1));
-#pragma unroll
-                    for (int a = 0; a < FL; ++a)
-                        w[it][a] = ld_sc1(src + (size_t)rs::wrapi(i - HALF + a + ox, X) * Y);
-                }
-            float ring[FL];
-#pragma unroll
-            for (int it = 0; it < PS_NL; ++it) {
-                if (it >= nL) continue;
-                const float* f = filt + (size_t)cfi[rs::wrapi(o0 - HALF + it, TH)] * FT;
-                float acc = 0.f;
-#pragma unroll
-                for (int a = 0; a < FL; ++a)
-#pragma unroll
-                    for (int t = 0; t < FL; ++t) acc += wave_rot(w[it][a], t - HALF) * f[a * FL + t];
-                ring[it % FL] = acc > 0.f ? acc : 0.f;
-                if (it >= 2 * HALF) {
-                    const int o = o0 + it - 2 * HALF;
-                    float v = 0.f;
-#pragma unroll
-                    for (int z = 0; z < FL; ++z) v += ring[(it + 1 + z) % FL] * zf[z];
-                    v = v > 0.f ? v : 0.f;
-                    if (tot != 0.0) v = v / tt;
-                    st_sc1(P + (size_t)o * LS + (size_t)i * Y + lane, v);
-                    const unsigned lin = ((unsigned)i * Y + lane) * TH + o;
-                    if (v > bv || (v == bv && lin < bl)) {
-                        bv = v;
-                        bl = lin;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            const float ov = __shfl_xor(bv, off);
-            const unsigned ol = __shfl_xor(bl, off);
-            if (ov > bv || (ov == bv && ol < bl)) {
-                bv = ov;
-                bl = ol;
-            }
-        }
-        if (lane == 0) {
-            s_bv[wave] = bv;
-            s_bl[wave] = bl;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < PS_NT / 64; ++w)
-                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
-                    bv = s_bv[w];
-                    bl = s_bl[w];
-                }
-            if (bl != 0xFFFFFFFFu)
-                atomicMax(res + (size_t)s * RES_SLOTS + (rank & (RES_SLOTS - 1)), argmax_key(bv, bl));
-        }
-        target += np;
-        ps_barrier(sync, target);
-    }
-}
-
 // Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
 // pinned host buffer (system-scope stores): one queued launch in place of a
 // device-to-host blit copy, which trailed the step by ~10 us (gap + copy kernel).
@@ -1564,9 +1293,6 @@ struct rs_pc {
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
-    bool persist = false;   // persistent one-XCD form for batched runs (RS_PC_FORM=persist)
-    int persistXcds = 1;    // XCDs it runs on (RS_PC_FORM=persist:K)
-    PsSync* dSync = nullptr;
     // odometry -> control tables (rs_pc_set_odometry_tables) and per-call scratch
     bool odoReady = false;
     OdoTables odo{};
@@ -1788,23 +1514,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     }
     if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
     if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
-    const bool persist = h->persist && !inline_ctl;
-    if (persist) {
-        // the whole batch in one launch on one XCD (pc_persist_kernel)
-        int cus = 0;
-        RS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
-        RS_HIP(hipMemsetAsync(h->dRes, 0, sizeof(unsigned long long) * RES_SLOTS * n, h->stream));
-        RS_HIP(hipMemsetAsync(h->dSync, 0, sizeof(PsSync), h->stream));
-        if (h->profiling) RS_HIP(hipEventRecord(h->evPool[0], h->stream));
-        hipLaunchKernelGGL(pc_persist_kernel, dim3(cus), dim3(PS_NT), 0, h->stream,
-                           static_cast<float*>(h->dP), static_cast<float*>(h->dQ), h->dPart, h->dCtl,
-                           h->ctlStride, ctl_off_oy(h), ctl_off_f(h), ctl_off_zf(h),
-                           static_cast<const float*>(h->dFilt), h->kf, h->dRes, n, h->X, h->TH,
-                           h->persistXcds, h->dSync);
-        RS_HIP(hipGetLastError());
-        if (h->profiling) RS_HIP(hipEventRecord(h->evPool[1], h->stream));
-    }
-    for (int s = 0; s < n && !persist; ++s) {
+    for (int s = 0; s < n; ++s) {
         const int pb = h->profiling ? 4 * s : -1;
         if (inline_ctl) {
             PcCtlInline c;
@@ -1833,18 +1543,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     RS_HIP(hipStreamSynchronize(h->stream));
     if (h->profiling) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     else h->lastMs = 0.f;  // the step-bracketing events are recorded only while profiling
-    if (persist) {
-        PsSync st{};
-        RS_HIP(hipMemcpy(&st, h->dSync, sizeof(st), hipMemcpyDeviceToHost));
-        RS_CHECK(st.count > 0 && st.timeout == 0, RS_ERR_HIP,
-                 "persistent step: %u participating blocks, timeout %u", st.count, st.timeout);
-    }
-    if (h->profiling && persist) {
-        float a = 0.f;
-        RS_HIP(hipEventElapsedTime(&a, h->evPool[0], h->evPool[1]));
-        h->kernelMs[0] = a;   // both phases of every step in one kernel
-        h->kernelMs[1] = 0.0;
-    } else if (h->profiling) {
+    if (h->profiling) {
         h->kernelMs[0] = h->kernelMs[1] = 0.0;
         for (int s = 0; s < n; ++s) {
             float a = 0.f, b = 0.f;
@@ -1972,15 +1671,6 @@ int pc_choose_form(rs_pc* h) {
         h->streamed = false;
         return RS_OK;
     }
-    if (env && std::strncmp(env, "persist", 7) == 0) {
-        if (env[7] == ':') h->persistXcds = std::max(1, std::min(8, std::atoi(env + 8)));
-        // batched runs in one launch on one XCD; single steps (update()) keep the rows form
-        RS_CHECK(h->esz == 4 && h->Y == 64 && h->TH >= FL && h->X >= HALF, RS_ERR_ARG,
-                 "RS_PC_FORM=persist needs float32, Y == 64 and TH >= 7");
-        h->streamed = false;
-        h->persist = true;
-        return RS_OK;
-    }
     if (env && std::strcmp(env, "tiles") == 0) {
         h->streamed = false;
         h->tiling = 0;
@@ -1992,7 +1682,7 @@ int pc_choose_form(rs_pc* h) {
         RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | persist | tiles | stream[:BX,WR,WC[,KC]])", env);
+                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
@@ -2116,12 +1806,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     PC_ALLOC(hipMalloc(&h->dP, h->n * h->esz));
     PC_ALLOC(hipMalloc(&h->dQ, h->n * h->esz));
     PC_ALLOC(hipMemsetAsync(h->dP, 0, h->n * h->esz, h->stream));  // zeros(shape), :27
-    PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * std::max(h->nPart, 1024)));  // persist: one per block
+    PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
     PC_ALLOC(hipMalloc(&h->dScalar, sizeof(double)));
-    if (h->persist) PC_ALLOC(hipMalloc(&h->dSync, sizeof(PsSync)));
     PC_ALLOC(hipMalloc(&h->dFilt, h->esz * FT * h->nf));
     if (h->prec == RS_PREC_F32) {
         std::vector<float> f(FT * (size_t)h->nf);
@@ -2151,7 +1840,7 @@ int rs_pc_destroy(rs_pc* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
-                    (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar, (void*)h->dSync})
+                    (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
         if (p) (void)hipFree(p);
     if (h->hRes) (void)hipHostFree(h->hRes);
     if (h->hCtl) (void)hipHostFree(h->hCtl);
@@ -2410,7 +2099,6 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
 const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
     if (h->streamed) return "stream";
-    if (h->persist) return "persist";
     return h->tiling ? "rows" : "tiles";
 }
 

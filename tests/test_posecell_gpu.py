@@ -218,31 +218,6 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
             net.close()
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 36), (16, 64, 10), (40, 64, 13), (100, 64, 9), (7, 64, 7)])
-def test_persistent_form_agrees_with_oracle(pcn, monkeypatch, shape):
-    """RS_PC_FORM=persist: a batch of steps in one launch on one XCD (two in-launch
-    barriers per step); grids with fewer x rows than blocks, ragged row bands and
-    theta chunks; a single update() on the same handle takes the rows kernels."""
-    monkeypatch.setenv('RS_PC_FORM', 'persist')
-    od = odometry(12, 23)
-    loc = tuple(s // 2 for s in shape)
-    ref = P.PoseCellOracle(shape)
-    ref.inject(1, loc)
-    maxes = [ref.update(v) for v in od]
-    net = pcn(shape)
-    assert net.step_form() == 'persist'
-    net.inject(1, loc)
-    got = net.run(od[:11])
-    assert [tuple(m) for m in got] == maxes[:11], shape
-    assert net.update(od[11]) == maxes[11]
-    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL, shape
-    got = net.run(od[:0])
-    assert got.shape == (0, 3)
-    net.close()
-    with pytest.raises(ValueError):
-        pcn(shape, precision='float64')
-
-
 def test_default_form_by_grid_size(pcn, monkeypatch):
     monkeypatch.delenv('RS_PC_FORM', raising=False)
     assert pcn((64, 64, 36)).step_form() == 'rows'
