@@ -1071,6 +1071,366 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     PC_STAMP(3, 4);
 }
 
+// ---------------------------------------------------------------------------
+// Column forms (large grids).  A block of CO_NW waves owns a TX x TY tile of
+// cells through ALL TH layers, so neither theta pass needs halo layers and no
+// layer waits on another: the block loads its whole (TX+6) x (TY+6) x TH window
+// at once (every load in flight together, one global round trip), then runs each
+// pass over all layers in parallel with one barrier between passes.  The xy halo
+// is re-read by neighbouring tiles ((TX+6)(TY+6) / (TX*TY) loads per cell) and
+// the y pass runs over the TX+6 window rows; the theta passes are not repeated.
+// The stream form's walk over KC+6 layers in sequence (one barrier and one LDS
+// round trip chain per layer) is what bounds it at 128x128x72; here a block has
+// four phases whatever TH is.  Tiles are numbered XCD-aware (st_tile).
+// Window rows/cols wrap with one conditional add/subtract, so X >= TX+6 and
+// Y >= TY+6 (checked on the host); TH <= co_thmax (the window in LDS).
+// ---------------------------------------------------------------------------
+#ifndef PC_CO_NW
+#define PC_CO_NW 9
+#endif
+#ifndef PC_CO_TX
+#define PC_CO_TX 8
+#endif
+// 9 waves: TH*TY = 576 x-pass tasks at TH = 72 (-D overrides for A/B builds of the probe)
+constexpr int CO_TX = PC_CO_TX, CO_TY = 8, CO_NW = PC_CO_NW;
+constexpr int CO_CH = 8;                        // layers per theta-pass task
+constexpr int CO_LDS = 150 * 1024;              // LDS budget of the excitation kernel
+// Window rows are loaded as 16-byte vectors of VEC = 16 / sizeof(T) cells from a
+// VEC-aligned start (Y % VEC == 0, so a vector never straddles the wrap): a row of
+// HY cells starting d = start % VEC cells into its first vector takes
+// ceil((HY + d) / VEC) vectors.  The excitation window starts at y0 - 3 with y0 a
+// multiple of 8 (d = VEC - 3 % VEC); the path windows are shifted per layer (any d).
+template <typename T>
+__host__ __device__ constexpr int co_vec() { return 16 / (int)sizeof(T); }
+template <typename T, bool SHIFTED>
+__host__ __device__ constexpr int co_ncp() {  // vectors per window row
+    return (CO_TY + 2 * HALF + (SHIFTED ? co_vec<T>() - 1 : (co_vec<T>() - HALF % co_vec<T>()) % co_vec<T>()) +
+            co_vec<T>() - 1) / co_vec<T>();
+}
+template <typename T>
+__host__ __device__ constexpr int co_thmax() {
+    return CO_LDS / (int)(((CO_TX + 2 * HALF) * (co_ncp<T, false>() + 1) * co_vec<T>() +
+                           2 * (CO_TX + 2 * HALF) * CO_TY) * sizeof(T));
+}
+
+// window coordinate a in [-n, 2n) -> [0, n)
+__device__ inline int co_wrap(int a, int n) {
+    a += a < 0 ? n : 0;
+    return a - (a >= n ? n : 0);
+}
+
+template <typename T>
+struct CoVec;
+template <>
+struct CoVec<float> { using type = float4; };
+template <>
+struct CoVec<double> { using type = double2; };
+
+// The TH x HX x NCP vectors of a column window -> LDS s_in[L][r][PV * VEC] (all
+// loads in flight together; rows PV >= NCP vectors apart).  Row r of layer L
+// starts at cell column (y0 - 3 + oy[L]) % Y, d[L] cells into its first vector.
+template <typename T, int NT, int HX, int NCP, int THM>
+struct CoWindow {
+    using V = typename CoVec<T>::type;
+    static constexpr int VEC = co_vec<T>(), LPT = (THM * HX * NCP + NT - 1) / NT;
+};
+
+template <typename T, int NT, int HX, int NCP, bool SHIFTED, typename V, int LPT>
+__device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, int Y, int TH, int x0,
+                                int y0, const int* s_ox, const int* s_oy) {
+    constexpr int VEC = co_vec<T>();
+    const int n = TH * HX * NCP, tid = threadIdx.x;
+    const size_t lstride = (size_t)X * Y;
+#pragma clang loop unroll(full)
+    for (int u = 0; u < LPT; ++u) {
+        const int e = min(tid + u * NT, n - 1), row = e / NCP, j = e - row * NCP;
+        const int L = row / HX, r = row - L * HX;
+        int gr = co_wrap(x0 - HALF + r, X), gc = co_wrap(y0 - HALF, Y);
+        if constexpr (SHIFTED) {
+            gr += s_ox[L];
+            gr -= gr >= X ? X : 0;
+            gc += s_oy[L];
+            gc -= gc >= Y ? Y : 0;
+        }
+        // first vector at gc rounded down to VEC; vector j wraps as a unit
+        w[u] = *reinterpret_cast<const V*>(src + L * lstride + (size_t)gr * Y +
+                                           co_wrap((gc & ~(VEC - 1)) + j * VEC, Y));
+    }
+}
+
+template <int NT, int HX, int NCP, int PV, typename T, typename V, int LPT>
+__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, int TH) {
+    const int n = TH * HX * NCP, tid = threadIdx.x;
+#pragma clang loop unroll(full)
+    for (int u = 0; u < LPT; ++u) {
+        const int e = tid + u * NT, row = e / NCP;
+        if (e < n) reinterpret_cast<V*>(s_in)[row * PV + e - row * NCP] = w[u];
+    }
+}
+
+// Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
+// (:339-340) and the normalisation partial sum (:343) for one column tile.
+template <typename T, int TX, int TY, int NW>
+__global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ P, T* __restrict__ Q,
+                                                          double* __restrict__ part,
+                                                          unsigned long long* __restrict__ res_slot,
+                                                          int X, int Y, int TH, int gx, SepKernel<T> k) {
+    constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
+    // rows one vector longer than they need: a lane per row reads its row as 16-byte
+    // vectors, and the odd pitch (in vectors) spreads those lanes over all banks
+    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, false>(), PV = NCP + 1, RP = PV * VEC, WN = HX * RP;
+    constexpr int D = (VEC - HALF % VEC) % VEC;  // window column 0 within its row's first vector
+    constexpr int THM = co_thmax<T>();
+    static_assert(2 * TX * TY <= WN, "x-pass outputs alias the window");
+    static_assert(TY % VEC == 0 && D + HY <= NCP * VEC, "window row layout");
+    __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] window; then the x-pass outputs
+    __shared__ T s_ye[THM * HX * TY];
+    __shared__ T s_yi[THM * HX * TY];
+    __shared__ double s_red[NW];
+    const int tid = threadIdx.x;
+    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int x0 = (tile % gx) * TX, y0 = (tile / gx) * TY;
+    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
+        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+    PC_STAMP(5, 0);
+    {
+        typename CoVec<T>::type win[CoWindow<T, NT, HX, NCP, THM>::LPT];
+        co_issue<T, NT, HX, NCP, false>(win, P, X, Y, TH, x0, y0, nullptr, nullptr);
+        co_store<NT, HX, NCP, PV>(win, s_in, TH);
+    }
+    __syncthreads();
+    PC_STAMP(5, 1);
+    // y pass: task (L, r) -> TY outputs of both Gaussians from one HY-wide window row
+    for (int t = tid; t < TH * HX; t += NT) {
+        using V = typename CoVec<T>::type;
+        T v[NCP * VEC];
+#pragma unroll
+        for (int j = 0; j < NCP; ++j) {
+            const V x = reinterpret_cast<const V*>(s_in + t * RP)[j];
+            if constexpr (VEC == 4) {
+                v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
+            } else {
+                v[2 * j] = x.x; v[2 * j + 1] = x.y;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < TY; ++c) {
+            T e = 0, g = 0;
+#pragma unroll
+            for (int q = 0; q < FL; ++q) {
+                e += k.ge[q] * v[D + c + q];
+                g += k.gi[q] * v[D + c + q];
+            }
+            s_ye[t * TY + c] = e;
+            s_yi[t * TY + c] = g;
+        }
+    }
+    __syncthreads();
+    PC_STAMP(5, 2);
+    // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows
+    T* s_xe = s_in;
+    T* s_xi = s_in + TH * TX * TY;
+    for (int t = tid; t < TH * TY; t += NT) {
+        const int L = t / TY, c = t - L * TY;
+        T ye[HX], yi[HX];
+#pragma unroll
+        for (int a = 0; a < HX; ++a) {
+            ye[a] = s_ye[(L * HX + a) * TY + c];
+            yi[a] = s_yi[(L * HX + a) * TY + c];
+        }
+#pragma unroll
+        for (int i = 0; i < TX; ++i) {
+            T e = 0, g = 0;
+#pragma unroll
+            for (int q = 0; q < FL; ++q) {
+                e += k.ge[q] * ye[i + q];
+                g += k.gi[q] * yi[i + q];
+            }
+            s_xe[(L * TX + i) * TY + c] = e;
+            s_xi[(L * TX + i) * TY + c] = g;
+        }
+    }
+    __syncthreads();
+    PC_STAMP(5, 3);
+    // theta pass: task (cell p, chunk j) -> CO_CH layers of one cell from CO_CH + 6
+    // x-pass layers (lanes <-> cells: a wave reads 64 consecutive LDS words)
+    double sum = 0.0;
+    const int nch = (TH + CO_CH - 1) / CO_CH;
+    for (int t = tid; t < TX * TY * nch; t += NT) {
+        const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
+        const int gi = x0 + i, gy = y0 + p - i * TY;
+        T xe[CO_CH + 2 * HALF], xi[CO_CH + 2 * HALF];
+#pragma unroll
+        for (int a = 0; a < CO_CH + 2 * HALF; ++a) {
+            const int L = co_wrap(j * CO_CH - HALF + a, TH);
+            xe[a] = s_xe[L * TX * TY + p];
+            xi[a] = s_xi[L * TX * TY + p];
+        }
+        const bool mine = gi < X && gy < Y;
+#pragma unroll
+        for (int o = 0; o < CO_CH; ++o) {
+            const int gk = j * CO_CH + o;
+            T e = 0, g = 0;
+#pragma unroll
+            for (int q = 0; q < FL; ++q) {
+                e += k.ge[q] * xe[o + q];
+                g += k.gi[q] * xi[o + q];
+            }
+            const T v = (e - g) * k.scale;
+            const T qv = (v < k.inhib) ? T(0) : v - k.inhib;
+            if (mine && gk < TH) {
+                Q[((size_t)gk * X + gi) * Y + gy] = qv;
+                sum += (double)qv;
+            }
+        }
+    }
+    sum = block_sum_w<NW>(sum, s_red);
+    if (tid == 0) part[blockIdx.x] = sum;
+    PC_STAMP(5, 4);
+}
+
+// Path integration (posecell_network.py:252-314) for one column tile: per-layer
+// shifted 7x7 filter (:273 -> convolution.py:320-340), clamp (:300), 7-tap theta
+// filter (:310 -> convolution.py:344-359), clamp (:314), normalisation by the
+// excitation total (:343-345, applied at the end), fused argmax (:317-319).
+template <typename T, int TX, int TY, int NW, typename CTL>
+__global__ __launch_bounds__(64 * NW) void pc_path_cols(
+    const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
+    const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
+    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx) {
+    constexpr int NT = 64 * NW, HX = TX + 2 * HALF;
+    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, true>(), RP = NCP * VEC, WN = HX * RP;
+    constexpr int THM = co_thmax<T>();
+    __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] shifted windows
+    __shared__ T s_p[THM * TX * TY];   // clamped 7x7 outputs [L][i][c]
+    __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
+    __shared__ int s_ox[THM], s_oy[THM], s_fo[THM];
+    __shared__ double s_red[NW];
+    __shared__ T s_bv[NW];
+    __shared__ unsigned s_bl[NW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int x0 = (tile % gx) * TX, y0 = (tile / gx) * TY;
+    PC_STAMP(6, 0);
+    // the normalisation partials' loads first, beside the control loads (a window
+    // held in registers across the reduction's barrier spills at 3 waves per SIMD,
+    // so the total is formed before the window loads are issued)
+    double tot = 0.0;
+    for (int i = tid; i < npart; i += NT) tot += part[i];
+    for (int L = tid; L < TH; L += NT) {
+        s_ox[L] = rs::wrapi(ctl_ox(ctl, L), X);  // shifts may exceed the grid (vtrans large)
+        s_oy[L] = rs::wrapi(ctl_oy(ctl, L), Y);
+        s_fo[L] = ctl_fi(ctl, L) * ST_FTP;
+    }
+    for (int i = tid; i < nf * FT; i += NT) {
+        const int fi = i / FT;
+        s_ftab[fi * ST_FTP + (i - fi * FT)] = filt[i];
+    }
+    T zf[FL];
+#pragma unroll
+    for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
+    tot = block_sum_w<NW>(tot, s_red);  // its barrier also publishes the control
+    const T tt = (T)tot;
+    PC_STAMP(6, 1);
+    // window (L, r, c) <-> Q[L][(x0-3+r+ox[L]) % X][(y0-3+c+oy[L]) % Y], at LDS column
+    // c + d[L] of row (L, r), d[L] = (y0 - 3 + oy[L]) % Y % VEC
+    typename CoVec<T>::type win[CoWindow<T, NT, HX, NCP, THM>::LPT];
+    co_issue<T, NT, HX, NCP, true>(win, Q, X, Y, TH, x0, y0, s_ox, s_oy);
+    co_store<NT, HX, NCP, NCP>(win, s_in, TH);
+    __syncthreads();
+    PC_STAMP(6, 2);
+    // 7x7 filter: task (L, c, half) -> TX/2 outputs of a column from TX/2 + 6 window
+    // rows (a whole column's filter taps + rows would spill at 3 waves per SIMD)
+    constexpr int TXH = TX / 2;
+    static_assert(TX % 2 == 0, "column halves");
+    for (int t = tid; t < TH * TY * 2; t += NT) {
+        const int L = t / (2 * TY), rem = t - L * 2 * TY, hf = rem / TY, c = rem - hf * TY;
+        T f[FT];
+        st_filter<T>(s_ftab + s_fo[L], f);
+        T acc[TXH];
+#pragma unroll
+        for (int i = 0; i < TXH; ++i) acc[i] = 0;
+        const int d = (co_wrap(y0 - HALF, Y) + s_oy[L]) % Y & (VEC - 1);
+        const T* win = s_in + L * WN + hf * TXH * RP + d + c;
+#pragma unroll
+        for (int a = 0; a < TXH + 2 * HALF; ++a) {
+            T w[FL];
+#pragma unroll
+            for (int q = 0; q < FL; ++q) w[q] = win[a * RP + q];
+#pragma unroll
+            for (int i = 0; i < TXH; ++i) {
+                const int x = a - i;
+                if (x < 0 || x >= FL) continue;
+#pragma unroll
+                for (int q = 0; q < FL; ++q) acc[i] += w[q] * f[x * FL + q];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TXH; ++i)
+            s_p[(L * TX + hf * TXH + i) * TY + c] = acc[i] > T(0) ? acc[i] : T(0);
+    }
+    __syncthreads();
+    PC_STAMP(6, 3);
+    // theta pass, clamp, normalisation, argmax: task (cell p, chunk j)
+    T bv = T(-1);
+    unsigned bl = 0xFFFFFFFFu;
+    const int nch = (TH + CO_CH - 1) / CO_CH;
+    for (int t = tid; t < TX * TY * nch; t += NT) {
+        const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
+        const int gi = x0 + i, gy = y0 + p - i * TY;
+        T r[CO_CH + 2 * HALF];
+#pragma unroll
+        for (int a = 0; a < CO_CH + 2 * HALF; ++a)
+            r[a] = s_p[co_wrap(j * CO_CH - HALF + a, TH) * TX * TY + p];
+        const bool mine = gi < X && gy < Y;
+#pragma unroll
+        for (int o = 0; o < CO_CH; ++o) {
+            const int gk = j * CO_CH + o;
+            T v = 0;
+#pragma unroll
+            for (int z = 0; z < FL; ++z) v += r[o + z] * zf[z];
+            v = v > T(0) ? v : T(0);
+            if (tot != 0.0) v = v / tt;
+            if (mine && gk < TH) {
+                P[((size_t)gk * X + gi) * Y + gy] = v;
+                const unsigned lin = ((unsigned)gi * Y + gy) * TH + gk;
+                if (v > bv || (v == bv && lin < bl)) {
+                    bv = v;
+                    bl = lin;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const T ov = __shfl_xor(bv, off);
+        const unsigned ol = __shfl_xor(bl, off);
+        if (ov > bv || (ov == bv && ol < bl)) {
+            bv = ov;
+            bl = ol;
+        }
+    }
+    if (lane == 0) {
+        s_bv[wave] = bv;
+        s_bl[wave] = bl;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int w = 1; w < NW; ++w)
+            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                bv = s_bv[w];
+                bl = s_bl[w];
+            }
+        if constexpr (sizeof(T) == 4) {
+            atomicMax(res_slot + (blockIdx.x & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
+        } else {
+            bmax[blockIdx.x] = bv;
+            bidx[blockIdx.x] = bl;
+        }
+    }
+    PC_STAMP(6, 4);
+}
+
 // Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
 // pinned host buffer (system-scope stores): one queued launch in place of a
 // device-to-host blit copy, which trailed the step by ~10 us (gap + copy kernel).
@@ -1291,6 +1651,8 @@ struct rs_pc {
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
+    bool cols = false;      // column kernels (RS_PC_FORM=cols): TX x TY tiles through all layers
+    int cgx = 0, cgy = 0;   // column tiles along x and y
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
     // odometry -> control tables (rs_pc_set_odometry_tables) and per-call scratch
@@ -1448,7 +1810,18 @@ int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     unsigned* bidx = h->dArgI ? h->dArgI + (size_t)s * h->nPathBlocks : nullptr;
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
-    if (h->streamed) {
+    if (h->cols) {
+        const dim3 g(h->cgx * h->cgy), b(64 * CO_NW);
+        hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW>), g, b, 0, h->stream, P, Q, h->dPart,
+                           slot, h->X, h->Y, h->TH, h->cgx, k);
+        RS_HIP(hipGetLastError());
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
+        if (!ctl) return RS_OK;
+        if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
+        hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW, CTL>), g, b, 0, h->stream, Q,
+                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot, bmax,
+                           bidx, h->X, h->Y, h->TH, h->cgx);
+    } else if (h->streamed) {
         RS_TRY((pc_launch_stream<T, CTL>(h, P, Q, slot, bmax, bidx, ctl, prof_base)));
     } else if (h->tiling == 64 || h->tiling == 128) {
         const dim3 g((h->X + RT_BX - 1) / RT_BX, (h->TH + RT_BK - 1) / RT_BK);
@@ -1663,6 +2036,15 @@ int pc_stream_scratch(int bx, int wr, int wc, size_t* bytes) {
     return RS_OK;
 }
 
+// The column kernels' limits: single-conditional wraps, the window in LDS, the
+// filter table in LDS.
+bool pc_cols_fit(const rs_pc* h) {
+    const int thmax = h->esz == 4 ? co_thmax<float>() : co_thmax<double>();
+    const int vec = h->esz == 4 ? co_vec<float>() : co_vec<double>();
+    return h->X >= CO_TX + 2 * HALF && h->Y >= CO_TY + 2 * HALF + 4 && h->Y % vec == 0 &&
+           h->TH >= CO_CH + 2 && h->TH <= thmax && h->nf <= RT_NFMAX;
+}
+
 int pc_choose_form(rs_pc* h) {
     int bx = 1, wr = 8, wc = 1, kc = 0;
     const char* env = std::getenv("RS_PC_FORM");
@@ -1676,13 +2058,25 @@ int pc_choose_form(rs_pc* h) {
         h->tiling = 0;
         return RS_OK;
     }
+    if (env && std::strcmp(env, "cols") == 0) {
+        RS_CHECK(pc_cols_fit(h), RS_ERR_ARG,
+                 "RS_PC_FORM=cols needs X >= %d, Y >= %d and a multiple of %d, %d <= TH <= %d and at "
+                 "most %d path filters",
+                 CO_TX + 2 * HALF, CO_TY + 2 * HALF + 4, h->esz == 4 ? co_vec<float>() : co_vec<double>(),
+                 CO_CH + 2, h->esz == 4 ? co_thmax<float>() : co_thmax<double>(), RT_NFMAX);
+        h->streamed = false;
+        h->cols = true;
+        h->cgx = (h->X + CO_TX - 1) / CO_TX;
+        h->cgy = (h->Y + CO_TY - 1) / CO_TY;
+        return RS_OK;
+    }
     const bool explicit_stream = env && std::strncmp(env, "stream:", 7) == 0;
     if (explicit_stream) {
         const int n = std::sscanf(env + 7, "%d,%d,%d,%d", &bx, &wr, &wc, &kc);
         RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | tiles | stream[:BX,WR,WC[,KC]])", env);
+                 "unknown RS_PC_FORM '%s' (rows | tiles | cols | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
@@ -1779,7 +2173,10 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         delete h;
         return st;
     }
-    if (h->streamed) {
+    if (h->cols) {
+        h->nPart = h->cgx * h->cgy;
+        h->nPathBlocks = h->nPart;
+    } else if (h->streamed) {
         h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;
         h->nPathBlocks = h->nPart;
     } else if (h->tiling) {
@@ -2099,6 +2496,7 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
 const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
     if (h->streamed) return "stream";
+    if (h->cols) return "cols";
     return h->tiling ? "rows" : "tiles";
 }
 

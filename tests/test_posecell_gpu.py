@@ -190,12 +190,21 @@ def test_simulate_driver(pcn):
 
 
 # every step-kernel form (RS_PC_FORM) against the oracle: the row-tiled and 3-D
-# tiled single-pass forms and the layer-streaming form at several tile shapes
+# tiled single-pass forms, the column form and the layer-streaming form at several tile shapes
 # (rows per wave, row groups, layers per block), incl. ragged tiles and grids
 # whose theta extent is not a multiple of the chunk
-FORMS = {'float32': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
+FORMS = {'float32': ['rows', 'tiles', 'cols', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
                      'stream:1,4,2,3', 'stream:2,4,2,6'],
-         'float64': ['rows', 'tiles', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
+         'float64': ['rows', 'tiles', 'cols', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
+
+
+def cols_fit(shape, precision):
+    """The column form's limits (posecell.hip pc_cols_fit): 16-byte row vectors
+    (Y a multiple of 4 cells at float32, 2 at float64), single-wrap halos, the
+    whole theta extent in LDS."""
+    X, Y, TH = shape
+    vec, thmax = (4, 76) if precision == 'float32' else (2, 42)
+    return X >= 14 and Y >= 18 and Y % vec == 0 and 10 <= TH <= thmax
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
@@ -209,6 +218,10 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
         want = ref.posecells
         for form in FORMS[precision]:
             monkeypatch.setenv('RS_PC_FORM', form)
+            if form == 'cols' and not cols_fit(shape, precision):
+                with pytest.raises(ValueError):
+                    pcn(shape, precision=precision)
+                continue
             net = pcn(shape, precision=precision)
             assert net.step_form() == form.split(':')[0]
             net.inject(1, loc)

@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     }
     rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
     unsigned long long* dbg;
-    const size_t ndbg = 5 * 4096 * 8;
+    const size_t ndbg = 7 * 4096 * 8;
     CK(hipMalloc(&dbg, ndbg * 8));
     CK(hipMemset(dbg, 0, ndbg * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
@@ -85,9 +85,11 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
     const int nb = h->nPart;
-    static const char* kname[4] = {"excite_rows", "path_rows", "excite_stream", "path_stream"};
-    static const int kns[4] = {4, 6, 5, 5};
-    for (int kid = 0; kid < 4; ++kid) {
+    static const char* kname[7] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
+                                   "excite_cols", "path_cols"};
+    static const int kns[7] = {4, 6, 5, 5, 0, 5, 5};
+    for (int kid = 0; kid < 7; ++kid) {
+        if (kid == 4) continue;  // shader-clock stamps, below
         const int ns = kns[kid];
         if (st[(size_t)kid * 4096 * 8] == 0) continue;  // kernel not used by this step form
         unsigned long long t0 = ~0ull, t1 = 0;
@@ -123,6 +125,41 @@ int main(int argc, char** argv) {
     if (h->streamed) {
         printf("stream tile BX=%d WR=%d KC=%d grid %d blocks\n", h->sbx, h->swr, h->sg.KC,
                h->sg.gx * h->sg.gy * h->sg.gz);
+        rs_pc_destroy(h);
+        return 0;
+    }
+    if (h->cols) {  // back-to-back launch costs of the column kernels
+        hipEvent_t c0, c1;
+        CK(hipEventCreate(&c0));
+        CK(hipEventCreate(&c1));
+        const dim3 g(h->cgx * h->cgy), b(64 * CO_NW);
+        const int reps = 500;
+        float t = 0;
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(empty_kernel, g, b, 0, h->stream, nullptr);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
+        const PcCtlRing ctl = make_ctl_ring(h, 0);
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW>), g, b, 0, h->stream,
+                               (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->cgx, h->kf);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, PcCtlRing>), g, b, 0, h->stream,
+                               (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
+                               (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
+                               (unsigned*)nullptr, X, Y, TH, h->cgx);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("path alone: %.2f us/launch\n", 1e3 * t / reps);
         rs_pc_destroy(h);
         return 0;
     }
