@@ -268,7 +268,7 @@ class PoseCellNetwork:
         return ms.value
 
     def step_form(self):
-        """Step kernels in use: 'rows' or 'tiles' (rs_pc_step_form)."""
+        """Step kernels in use: 'rows', 'tiles', 'cols' or 'stream' (rs_pc_step_form)."""
         return self._lib.rs_pc_step_form(self._h).decode()
 
     def set_profiling(self, enable=True):

@@ -234,7 +234,9 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
 def test_default_form_by_grid_size(pcn, monkeypatch):
     monkeypatch.delenv('RS_PC_FORM', raising=False)
     assert pcn((64, 64, 36)).step_form() == 'rows'
-    assert pcn((128, 128, 72)).step_form() == 'stream'
+    assert pcn((128, 128, 72)).step_form() == 'cols'
+    assert pcn((128, 130, 72)).step_form() == 'stream'    # Y not a multiple of 4: no cols
+    assert pcn((128, 128, 100)).step_form() == 'stream'   # theta extent beyond the LDS window
     monkeypatch.setenv('RS_PC_FORM', 'stream:3,8,1')
     with pytest.raises(ValueError):
         pcn((64, 64, 36))

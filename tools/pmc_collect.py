@@ -24,7 +24,7 @@ import os
 import re
 
 SCANS = {'headline': (1000, 10240), 'stress': (10000, 5120), 'library': (100000, 2048)}
-PCS = {'pc64': ('rows', [64, 64, 36]), 'pc128': ('stream', [128, 128, 72])}
+PCS = {'pc64': ('rows', [64, 64, 36]), 'pc128': ('cols', [128, 128, 72])}
 
 
 def short(name):
