@@ -389,13 +389,6 @@ constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
 #endif
 constexpr int PL_NB = PL_NB_Q;  // queries per LDS batch (staged planes; one reducing wave each)
 
-__device__ inline uint32_t plane_borrows(const uint32_t (&t)[8], const uint32_t* q) {
-    uint32_t b = __builtin_amdgcn_bitop3_b32(t[0], q[0], 0u, 0x8E);
-#pragma unroll
-    for (int k = 1; k < 8; ++k) b = __builtin_amdgcn_bitop3_b32(t[k], q[k], b, 0x8E);
-    return b;
-}
-
 // One block per stored template: planes + TS of raw template src[t] into slot dst[t].
 __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __restrict__ raw,
                                                              const int32_t* __restrict__ src,
@@ -567,37 +560,125 @@ __device__ __forceinline__ void plane_rows(const uint32_t (&P)[PlaneRange<H, HAL
     if constexpr (S < R::SB) plane_rows<H, HALF, S + 1>(P, sq, acc);
 }
 
+#ifndef PL_ONEBAR
+#define PL_ONEBAR 1
+#endif
+
 template <int H>
 struct PlaneLds {
     static constexpr int M = FAST_M, NS = H - 2 * M + 3, NO = 2 * M - 1, NK = (NO + 1) / 2;
     static constexpr int QW = PL_CG * NS * 8;                 // query-plane dwords per query
     static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
+#if PL_ONEBAR
+    // double-buffered: batch i computes from q[i&1] and adds its partial counts into
+    // part[i&1] while batch i+1 is staged into q[(i+1)&1]; one barrier per batch
+    uint4 q[2][PL_NB * QW / 4];
+    uint32_t part[2][PL_NB][NK][64];                           // u16 pairs, summed by ds_add
+    int bidx[3];                                               // batches taken ahead (ring)
+#else
     uint4 q[PL_NB * QW / 4];                                   // the batch's query planes
     uint32_t part[PL_NB][NK][NW][64];                          // u16 pairs: offsets 2k, 2k+1
-    uint32_t ts[16][64];                                       // TS(o) of the 64 templates
     int batch;
+#endif
+    uint32_t ts[16][64];                                       // TS(o) of the 64 templates
 };
 
+template <int H, int HALF>
+__device__ __forceinline__ void plane_load_units(const uint4* __restrict__ planes, int tb, int cg,
+                                                 int lane, uint32_t (&P)[PlaneRange<H, HALF>::NUH][8]) {
+    using R = PlaneRange<H, HALF>;
+    const uint4* src = planes + ((size_t)(tb * PL_CG + cg) * (H / 4) + R::JLO) * 128 + lane;
+#pragma unroll
+    for (int j = 0; j < R::NUH; ++j) {
+        const uint4 a = src[(2 * j) * 64], b = src[(2 * j + 1) * 64];
+        P[j][0] = a.x; P[j][1] = a.y; P[j][2] = a.z; P[j][3] = a.w;
+        P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
+    }
+}
+
+#if PL_ONEBAR
+// The work of one wave: column group cg, query start rows of range HALF.  One
+// barrier per batch: before it, every wave stages its share of the next batch's
+// planes and adds this batch's partial counts into LDS (ds_add; the per-half
+// sums stay < 2^16, so the packed pairs never carry); after it, wave w < nb
+// finishes query w of the batch and clears its partial slots for batch i+2.
+// Batches are taken one ahead by thread 0; a block stops taking after its first
+// failed take, so every block ends on exactly one failed take (counter rewind).
+template <int H, int HALF, bool MATRIX>
+__device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
+                                           int tb, int64_t count, const uint4* __restrict__ qp4,
+                                           const uint32_t* __restrict__ qsum, int nq,
+                                           unsigned* __restrict__ ctr, int G, int g, ScanOut out,
+                                           int rank, int nranks, int wave, int cg, int lane,
+                                           unsigned& failed) {
+    using R = PlaneRange<H, HALF>;
+    using LD = PlaneLds<H>;
+    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
+    uint32_t P[R::NUH][8];
+    plane_load_units<H, HALF>(planes, tb, cg, lane, P);
+    const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
+    const int64_t slot = (int64_t)tb * 64 + lane;
+    const int tid = wave * 64 + lane;
+    // batch ring: iteration it reads the next batch from slot (it+1) % 3 and thread
+    // 0 writes the one after it into slot (it+2) % 3, last read two barriers ago
+    int bi = L.bidx[0];
+    for (int it = 0;; ++it) {
+        if (bi >= nbatch) break;  // block-uniform
+        const int cur = it & 1, nxt = cur ^ 1, r1 = (it + 1) % 3, r2 = (it + 2) % 3;
+        const int bn = L.bidx[r1];
+        const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
+        if (bn < nbatch) {  // stage the next batch (its buffer's last readers passed the previous barrier)
+            const int qn = (bn * G + g) * PL_NB, nbn = min(PL_NB, nq - qn);
+            for (int i = tid; i < nbn * LD::QW / 4; i += NT) L.q[nxt][i] = qp4[(size_t)qn * (LD::QW / 4) + i];
+            if (tid == 0) {  // the batch after next
+                const unsigned t = atomicAdd(ctr, 1u);
+                L.bidx[r2] = (int)t;
+                if ((int)t >= nbatch) failed = t;
+            }
+        } else if (tid == 0) {
+            L.bidx[r2] = nbatch;  // no further take: this block's failed take was bn
+        }
+#pragma unroll 1
+        for (int b = 0; b < nb; ++b) {
+            uint32_t acc[NO];
+#pragma unroll
+            for (int o = 0; o < NO; ++o) acc[o] = 0u;
+            plane_rows<H, HALF, R::SA>(
+                P, reinterpret_cast<const uint32_t*>(L.q[cur]) + (b * PL_CG + cg) * NS * 8, acc);
+#pragma unroll
+            for (int k = 0; k < NK; ++k)
+                atomicAdd(&L.part[cur][b][k][lane], acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u));
+        }
+        __syncthreads();
+        if (wave < nb) {  // wave w finishes query qb + w of the batch
+            const int qi = qb + wave;
+            uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const uint32_t t = L.part[cur][wave][k][lane];
+                L.part[cur][wave][k][lane] = 0u;
+                best = min(best, L.ts[2 * k][lane] + 256u * (t & 0xFFFFu));
+                if (2 * k + 1 < NO) best = min(best, L.ts[2 * k + 1][lane] + 256u * (t >> 16));
+            }
+            emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
+        }
+        bi = bn;
+    }
+}
+#else
 // The work of one wave: column group cg, query start rows of range HALF.
 template <int H, int HALF, bool MATRIX>
 __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
                                            int tb, int64_t count, const uint4* __restrict__ qp4,
                                            const uint32_t* __restrict__ qsum, int nq,
                                            unsigned* __restrict__ ctr, int G, int g, ScanOut out,
-                                           int rank, int nranks, int wave, int cg, int lane) {
+                                           int rank, int nranks, int wave, int cg, int lane,
+                                           unsigned& failed) {
     using R = PlaneRange<H, HALF>;
     using LD = PlaneLds<H>;
     constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
     uint32_t P[R::NUH][8];
-    {
-        const uint4* src = planes + ((size_t)(tb * PL_CG + cg) * (H / 4) + R::JLO) * 128 + lane;
-#pragma unroll
-        for (int j = 0; j < R::NUH; ++j) {
-            const uint4 a = src[(2 * j) * 64], b = src[(2 * j + 1) * 64];
-            P[j][0] = a.x; P[j][1] = a.y; P[j][2] = a.z; P[j][3] = a.w;
-            P[j][4] = b.x; P[j][5] = b.y; P[j][6] = b.z; P[j][7] = b.w;
-        }
-    }
+    plane_load_units<H, HALF>(planes, tb, cg, lane, P);
     // this block's query group g of G: batches g, g + G, g + 2G, ...
     const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     const int64_t slot = (int64_t)tb * 64 + lane;
@@ -611,7 +692,10 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
         const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
         for (int i = tid; i < nb * LD::QW / 4; i += NT) L.q[i] = qp4[(size_t)qb * (LD::QW / 4) + i];
         __syncthreads();  // (A)
-        if (tid == 0) L.batch = (int)atomicAdd(ctr, 1u);
+        if (tid == 0) {
+            L.batch = (int)atomicAdd(ctr, 1u);
+            if (L.batch >= nbatch) failed = (unsigned)L.batch;
+        }
 #pragma unroll 1
         for (int b = 0; b < nb; ++b) {
             uint32_t acc[NO];
@@ -639,6 +723,7 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
         }
     }
 }
+#endif
 
 // nqc blocks serve each template block; they take query batches of PL_NB from
 // the template block's counter, so blocks that the SIMDs' oldest-first issue
@@ -662,20 +747,50 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     VT_STAMP(0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, cg = wave % PL_CG, half = wave / PL_CG;
+    const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
-    if (threadIdx.x == 0) L.batch = (int)atomicAdd(ctr, 1u);
+    unsigned failed = 0u;  // thread 0: the value of this block's one failed take
+#if PL_ONEBAR
+    for (int i = threadIdx.x; i < 2 * PL_NB * PlaneLds<H>::NK * 64; i += blockDim.x)
+        (&L.part[0][0][0][0])[i] = 0u;
+    if (threadIdx.x == 0) {  // the first batch and the one after it
+        const unsigned a = atomicAdd(ctr, 1u);
+        unsigned b = (unsigned)nbatch;
+        if ((int)a < nbatch) {
+            b = atomicAdd(ctr, 1u);
+            if ((int)b >= nbatch) failed = b;
+        } else {
+            failed = a;
+        }
+        L.bidx[0] = (int)a;
+        L.bidx[1] = (int)b;
+    }
+    __syncthreads();
+    if (L.bidx[0] < nbatch) {  // stage the first batch
+        constexpr int QW4 = PlaneLds<H>::QW / 4;
+        const int qb = (L.bidx[0] * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
+        const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
+        for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) L.q[0][i] = qp4[(size_t)qb * QW4 + i];
+    }
+#else
+    if (threadIdx.x == 0) {
+        L.batch = (int)atomicAdd(ctr, 1u);
+        if (L.batch >= nbatch) failed = (unsigned)L.batch;
+    }
+#endif
     __syncthreads();
     const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
     if (half == 0)
         plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
-                                 wave, cg, lane);
+                                 wave, cg, lane, failed);
     else
         plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
-                                 wave, cg, lane);
+                                 wave, cg, lane, failed);
     // Each of the nqc / G blocks sharing a counter ends on exactly one failed take, so
-    // the block whose take returned (group batches) + nqc / G - 1 is the counter's last
-    // user in this launch: it rewinds the counter for the next launch (no memset).
-    if (threadIdx.x == 0 && L.batch == ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G + nqc / G - 1) *ctr = 0u;
+    // the block whose failed take returned (group batches) + nqc / G - 1 is the
+    // counter's last user in this launch: it rewinds the counter for the next launch
+    // (no memset).
+    if (threadIdx.x == 0 && failed == (unsigned)(nbatch + nqc / G - 1)) *ctr = 0u;
     VT_STAMP(1);
 }
 
