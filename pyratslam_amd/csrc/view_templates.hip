@@ -385,7 +385,7 @@ constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
     } while (0)
 #endif
 #ifndef PL_NB_Q
-#define PL_NB_Q 2
+#define PL_NB_Q 4
 #endif
 constexpr int PL_NB = PL_NB_Q;  // queries per LDS batch (staged planes; one reducing wave each)
 
