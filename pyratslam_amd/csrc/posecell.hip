@@ -1116,11 +1116,20 @@ __host__ __device__ constexpr int co_ncp() {  // vectors per window row
     return (CO_TY + 2 * HALF + (SHIFTED ? co_vec<T>() - 1 : (co_vec<T>() - HALF % co_vec<T>()) % co_vec<T>()) +
             co_vec<T>() - 1) / co_vec<T>();
 }
+// Layers of LDS window per block: the whole theta extent in one block per CU
+// (co_thmax), or a theta chunk plus its 6 halo layers with two blocks per CU
+// (co_thmax_chunk).  The excitation kernel's window + y-pass outputs set the size.
 template <typename T>
-__host__ __device__ constexpr int co_thmax() {
-    return CO_LDS / (int)(((CO_TX + 2 * HALF) * (co_ncp<T, false>() + 1) * co_vec<T>() +
-                           2 * (CO_TX + 2 * HALF) * CO_TY) * sizeof(T));
+__host__ __device__ constexpr int co_layer_bytes(bool padded) {
+    return ((CO_TX + 2 * HALF) * (co_ncp<T, false>() + (padded ? 1 : 0)) * co_vec<T>() +
+            2 * (CO_TX + 2 * HALF) * CO_TY) * (int)sizeof(T);
 }
+template <typename T>
+__host__ __device__ constexpr int co_thmax() { return CO_LDS / co_layer_bytes<T>(true); }
+constexpr int CO_LDS_CHUNK = 76 * 1024;   // two blocks per CU
+constexpr int CO_NW_CHUNK = 8;            // 16 waves per CU: the path kernel's VGPRs allow 4 per SIMD
+template <typename T>
+__host__ __device__ constexpr int co_thmax_chunk() { return CO_LDS_CHUNK / co_layer_bytes<T>(false); }
 
 // Block barrier for LDS traffic only: waits for this wave's LDS operations, not
 // for its global stores (a __syncthreads fence would drain those too).
@@ -1188,11 +1197,47 @@ struct CoWindow {
     static constexpr int VEC = co_vec<T>(), LPT = (THM * HX * NCP + NT - 1) / NT;
 };
 
-template <typename T, int NT, int HX, int NCP, bool SHIFTED, typename V, int LPT>
-__device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, int Y, int TH, int x0,
-                                int y0, const int* s_ox, const int* s_oy) {
+// Layers of one column block: nl = nout + 2*halo window layers, local layer L
+// holding global layer k0 - halo + L (wrapped); CHUNK: the block holds a theta
+// chunk (halo 3), else the whole periodic extent (k0 = 0, nout = TH, halo 0).
+template <bool CHUNK>
+struct CoLayers {
+    int k0, nout, nl;
+    __device__ inline int global(int L, int TH) const { return CHUNK ? co_wrap(k0 - HALF + L, TH) : L; }
+    // local layer of theta tap a (0..13) for the outputs of chunk j (8 per task)
+    __device__ inline int tap(int j, int a, int TH) const {
+        return CHUNK ? min(j * 8 + a, nl - 1) : co_wrap(j * 8 - HALF + a, TH);
+    }
+};
+
+template <bool CHUNK>
+__device__ inline CoLayers<CHUNK> co_layers(int ch, int KC, int TH) {
+    CoLayers<CHUNK> c;
+    c.k0 = CHUNK ? ch * KC : 0;
+    c.nout = CHUNK ? min(KC, TH - c.k0) : TH;
+    c.nl = c.nout + (CHUNK ? 2 * HALF : 0);
+    return c;
+}
+
+// LDS vector slot of vector j of window row `row` (NCP vectors per row).  The
+// excitation window is read a row per lane as 16-byte vectors: with the whole
+// theta extent in LDS its rows are padded by one vector (odd pitch); a theta
+// chunk (two blocks per CU, no room for padding) XOR-swizzles the slots so 16
+// lanes reading 16 consecutive rows hit 16 distinct bank groups.  The path
+// window is plain.
+enum CoSlot { CO_PLAIN, CO_PADDED, CO_SWIZZLED };
+template <int NCP, int LAYOUT>
+__device__ inline int co_slot(int row, int j) {
+    if constexpr (LAYOUT == CO_SWIZZLED) return row * NCP + (j ^ ((row / (16 / NCP)) % NCP));
+    else if constexpr (LAYOUT == CO_PADDED) return row * (NCP + 1) + j;
+    else return row * NCP + j;
+}
+
+template <typename T, int NT, int HX, int NCP, bool SHIFTED, bool CHUNK, typename V, int LPT>
+__device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, int Y, int TH,
+                                const CoLayers<CHUNK>& ly, int x0, int y0, const int* s_ox, const int* s_oy) {
     constexpr int VEC = co_vec<T>();
-    const int n = TH * HX * NCP, tid = threadIdx.x;
+    const int n = ly.nl * HX * NCP, tid = threadIdx.x;
     const size_t lstride = (size_t)X * Y;
 #pragma clang loop unroll(full)
     for (int u = 0; u < LPT; ++u) {
@@ -1212,60 +1257,61 @@ __device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, i
         int jj = j;
         if constexpr (SHIFTED)
             jj = (j < NCP - 1 || (gc & (VEC - 1)) > (NCP - 1) * VEC - (2 * HALF + CO_TY)) ? j : 0;
-        w[u] = *reinterpret_cast<const V*>(src + L * lstride + (size_t)gr * Y +
+        w[u] = *reinterpret_cast<const V*>(src + (size_t)ly.global(L, TH) * lstride + (size_t)gr * Y +
                                            co_wrap((gc & ~(VEC - 1)) + jj * VEC, Y));
     }
 }
 
-template <int NT, int HX, int NCP, int PV, typename T, typename V, int LPT>
-__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, int TH) {
-    const int n = TH * HX * NCP, tid = threadIdx.x;
+template <int NT, int HX, int NCP, int LAYOUT, bool CHUNK, typename T, typename V, int LPT>
+__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly) {
+    const int n = ly.nl * HX * NCP, tid = threadIdx.x;
 #pragma clang loop unroll(full)
     for (int u = 0; u < LPT; ++u) {
         const int e = tid + u * NT, row = e / NCP;
-        if (e < n) reinterpret_cast<V*>(s_in)[row * PV + e - row * NCP] = w[u];
+        if (e < n) reinterpret_cast<V*>(s_in)[co_slot<NCP, LAYOUT>(row, e - row * NCP)] = w[u];
     }
 }
 
 // Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
 // (:339-340) and the normalisation partial sum (:343) for one column tile.
-template <typename T, int TX, int TY, int NW>
+template <typename T, int TX, int TY, int NW, int THM, bool CHUNK>
 __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ P, T* __restrict__ Q,
                                                           double* __restrict__ part,
                                                           unsigned long long* __restrict__ res_slot,
-                                                          int X, int Y, int TH, int gx, SepKernel<T> k) {
+                                                          int X, int Y, int TH, int gx, int gy, int KC,
+                                                          SepKernel<T> k) {
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
-    // rows one vector longer than they need: a lane per row reads its row as 16-byte
-    // vectors, and the odd pitch (in vectors) spreads those lanes over all banks
-    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, false>(), PV = NCP + 1, RP = PV * VEC, WN = HX * RP;
+    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, false>();
+    constexpr int LAYOUT = CHUNK ? CO_SWIZZLED : CO_PADDED, RP = (NCP + (CHUNK ? 0 : 1)) * VEC, WN = HX * RP;
     constexpr int D = (VEC - HALF % VEC) % VEC;  // window column 0 within its row's first vector
-    constexpr int THM = co_thmax<T>();
     static_assert(2 * TX * TY <= WN, "x-pass outputs alias the window");
     static_assert(TY % VEC == 0 && D + HY <= NCP * VEC, "window row layout");
     __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] window; then the x-pass outputs
     __shared__ T s_ye[THM * HX * TY];
     __shared__ T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
+    using V = typename CoVec<T>::type;
     const int tid = threadIdx.x;
-    const int tile = st_tile(blockIdx.x, gridDim.x);
-    const int x0 = (tile % gx) * TX, y0 = (tile / gx) * TY;
+    const int tile = st_tile(blockIdx.x, gridDim.x), xy = tile % (gx * gy);
+    const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
+    const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
         res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
     PC_STAMP(5, 0);
     {
-        typename CoVec<T>::type win[CoWindow<T, NT, HX, NCP, THM>::LPT];
-        co_issue<T, NT, HX, NCP, false>(win, P, X, Y, TH, x0, y0, nullptr, nullptr);
-        co_store<NT, HX, NCP, PV>(win, s_in, TH);
+        V win[CoWindow<T, NT, HX, NCP, THM>::LPT];
+        co_issue<T, NT, HX, NCP, false>(win, P, X, Y, TH, ly, x0, y0, nullptr, nullptr);
+        co_store<NT, HX, NCP, LAYOUT>(win, s_in, ly);
     }
     co_lds_barrier();
     PC_STAMP(5, 1);
-    // y pass: task (L, r) -> TY outputs of both Gaussians from one HY-wide window row
-    for (int t = tid; t < TH * HX; t += NT) {
-        using V = typename CoVec<T>::type;
+    // y pass: task (L, r) -> TY outputs of both Gaussians from one window row, read
+    // as NCP 16-byte vectors (padded or swizzled slots: conflict-free across lanes)
+    for (int t = tid; t < ly.nl * HX; t += NT) {
         T v[NCP * VEC];
 #pragma unroll
         for (int j = 0; j < NCP; ++j) {
-            const V x = reinterpret_cast<const V*>(s_in + t * RP)[j];
+            const V x = reinterpret_cast<const V*>(s_in)[co_slot<NCP, LAYOUT>(t, j)];
             if constexpr (VEC == 4) {
                 v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
             } else {
@@ -1288,8 +1334,8 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     PC_STAMP(5, 2);
     // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows
     T* s_xe = s_in;
-    T* s_xi = s_in + TH * TX * TY;
-    for (int t = tid; t < TH * TY; t += NT) {
+    T* s_xi = s_in + THM * TX * TY;
+    for (int t = tid; t < ly.nl * TY; t += NT) {
         const int L = t / TY, c = t - L * TY;
         T ye[HX], yi[HX];
 #pragma unroll
@@ -1311,24 +1357,24 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     }
     co_lds_barrier();
     PC_STAMP(5, 3);
-    // theta pass: task (cell p, chunk j) -> CO_CH layers of one cell from CO_CH + 6
-    // x-pass layers (lanes <-> cells: a wave reads 64 consecutive LDS words)
+    // theta pass: task (cell p, chunk j) -> CO_CH output layers of one cell from
+    // CO_CH + 6 x-pass layers (lanes <-> cells: a wave reads 64 consecutive LDS words)
     double sum = 0.0;
-    const int nch = (TH + CO_CH - 1) / CO_CH;
+    const int nch = (ly.nout + CO_CH - 1) / CO_CH;
     for (int t = tid; t < TX * TY * nch; t += NT) {
         const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
         const int gi = x0 + i, gy = y0 + p - i * TY;
         T xe[CO_CH + 2 * HALF], xi[CO_CH + 2 * HALF];
 #pragma unroll
         for (int a = 0; a < CO_CH + 2 * HALF; ++a) {
-            const int L = co_wrap(j * CO_CH - HALF + a, TH);
+            const int L = ly.tap(j, a, TH);
             xe[a] = s_xe[L * TX * TY + p];
             xi[a] = s_xi[L * TX * TY + p];
         }
         const bool mine = gi < X && gy < Y;
 #pragma unroll
         for (int o = 0; o < CO_CH; ++o) {
-            const int gk = j * CO_CH + o;
+            const int lo = j * CO_CH + o, gk = ly.k0 + lo;
             T e = 0, g = 0;
 #pragma unroll
             for (int q = 0; q < FL; ++q) {
@@ -1337,7 +1383,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             }
             const T v = (e - g) * k.scale;
             const T qv = (v < k.inhib) ? T(0) : v - k.inhib;
-            if (mine && gk < TH) {
+            if (mine && lo < ly.nout) {
 #ifndef PC_DIAG_NOSTORE  // diagnostic build of tools/pc_probe.hip only: no output stores
                 Q[((size_t)gk * X + gi) * Y + gy] = qv;
 #endif
@@ -1361,14 +1407,13 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
 // shifted 7x7 filter (:273 -> convolution.py:320-340), clamp (:300), 7-tap theta
 // filter (:310 -> convolution.py:344-359), clamp (:314), normalisation by the
 // excitation total (:343-345, applied at the end), fused argmax (:317-319).
-template <typename T, int TX, int TY, int NW, typename CTL>
+template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL>
 __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
     const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
-    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx) {
+    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx, int gy, int KC) {
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF;
     constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, true>(), RP = NCP * VEC, WN = HX * RP;
-    constexpr int THM = co_thmax<T>();
     __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] shifted windows
     __shared__ T s_p[THM * TX * TY];   // clamped 7x7 outputs [L][i][c]
     __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
@@ -1376,8 +1421,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     __shared__ T s_bv[NW];
     __shared__ unsigned s_bl[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tile = st_tile(blockIdx.x, gridDim.x);
-    const int x0 = (tile % gx) * TX, y0 = (tile / gx) * TY;
+    const int tile = st_tile(blockIdx.x, gridDim.x), xy = tile % (gx * gy);
+    const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
+    const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     PC_STAMP(6, 0);
     // the normalisation partials' loads first (vmcnt waits are in issue order, so
     // the reduction after the window loads are issued waits for these alone).
@@ -1387,11 +1433,12 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     double pt[NPL];
 #pragma unroll
     for (int u = 0; u < NPL; ++u) pt[u] = lane + 64 * u < npart ? part[lane + 64 * u] : 0.0;
-    for (int L = tid; L < TH; L += NT) {
-        s_ox[L] = rs::wrapi(ctl_ox(ctl, L), X);  // shifts may exceed the grid (vtrans large)
-        const int oy = rs::wrapi(ctl_oy(ctl, L), Y);
+    for (int L = tid; L < ly.nl; L += NT) {
+        const int gL = ly.global(L, TH);
+        s_ox[L] = rs::wrapi(ctl_ox(ctl, gL), X);  // shifts may exceed the grid (vtrans large)
+        const int oy = rs::wrapi(ctl_oy(ctl, gL), Y);
         s_oy[L] = oy;
-        s_fo[L] = ctl_fi(ctl, L) * ST_FTP;
+        s_fo[L] = ctl_fi(ctl, gL) * ST_FTP;
         // window row (L, r) starts this many cells into its first vector
         s_yd[L] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
     }
@@ -1407,14 +1454,14 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // window (L, r, c) <-> Q[L][(x0-3+r+ox[L]) % X][(y0-3+c+oy[L]) % Y], at LDS column
     // c + d[L] of row (L, r), d[L] = (y0 - 3 + oy[L]) % Y % VEC
     typename CoVec<T>::type win[CoWindow<T, NT, HX, NCP, THM>::LPT];
-    co_issue<T, NT, HX, NCP, true>(win, Q, X, Y, TH, x0, y0, s_ox, s_oy);
+    co_issue<T, NT, HX, NCP, true>(win, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < NPL; ++u) tot += pt[u];
     for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
     tot = co_wave_sum(tot);
     const T tt = (T)tot;
-    co_store<NT, HX, NCP, NCP>(win, s_in, TH);
+    co_store<NT, HX, NCP, CO_PLAIN>(win, s_in, ly);
     co_lds_barrier();
     PC_STAMP(6, 2);
     // 7x7 filter: task (L, column group, row part) -> TX/FS rows x CP columns of
@@ -1423,7 +1470,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // of them spills at 3 waves per SIMD)
     constexpr int FS = PC_CO_FSPLIT, TXH = TX / FS, CP = PC_CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    for (int t = tid; t < TH * NCG * FS; t += NT) {
+    for (int t = tid; t < ly.nl * NCG * FS; t += NT) {
         const int L = t / (FS * NCG), rem = t - L * FS * NCG, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
         T f[FT];
         st_filter<T>(s_ftab + s_fo[L], f);
@@ -1463,24 +1510,23 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
-    const int nch = (TH + CO_CH - 1) / CO_CH;
+    const int nch = (ly.nout + CO_CH - 1) / CO_CH;
     for (int t = tid; t < TX * TY * nch; t += NT) {
         const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
         const int gi = x0 + i, gy = y0 + p - i * TY;
         T r[CO_CH + 2 * HALF];
 #pragma unroll
-        for (int a = 0; a < CO_CH + 2 * HALF; ++a)
-            r[a] = s_p[co_wrap(j * CO_CH - HALF + a, TH) * TX * TY + p];
+        for (int a = 0; a < CO_CH + 2 * HALF; ++a) r[a] = s_p[ly.tap(j, a, TH) * TX * TY + p];
         const bool mine = gi < X && gy < Y;
 #pragma unroll
         for (int o = 0; o < CO_CH; ++o) {
-            const int gk = j * CO_CH + o;
+            const int lo = j * CO_CH + o, gk = ly.k0 + lo;
             T v = 0;
 #pragma unroll
             for (int z = 0; z < FL; ++z) v += r[o + z] * zf[z];
             v = v > T(0) ? v : T(0);
             if (tot != 0.0) v = v / tt;
-            if (mine && gk < TH) {
+            if (mine && lo < ly.nout) {
 #ifndef PC_DIAG_NOSTORE
                 P[((size_t)gk * X + gi) * Y + gy] = v;
 #endif
@@ -1751,8 +1797,9 @@ struct rs_pc {
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
-    bool cols = false;      // column kernels (RS_PC_FORM=cols): TX x TY tiles through all layers
+    bool cols = false;      // column kernels (RS_PC_FORM=cols[:KC]): TX x TY tiles through KC layers
     int cgx = 0, cgy = 0;   // column tiles along x and y
+    int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
     // odometry -> control tables (rs_pc_set_odometry_tables) and per-call scratch
@@ -1911,16 +1958,30 @@ int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->cols) {
-        const dim3 g(h->cgx * h->cgy), b(64 * CO_NW);
-        hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW>), g, b, 0, h->stream, P, Q, h->dPart,
-                           slot, h->X, h->Y, h->TH, h->cgx, k);
+        const dim3 g(h->cgx * h->cgy * h->coNch);
+        const bool whole = h->coKC >= h->TH;
+        constexpr int THF = co_thmax<T>(), THC = co_thmax_chunk<T>();
+        if (whole)
+            hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW, THF, false>), g, dim3(64 * CO_NW), 0,
+                               h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                               h->coKC, k);
+        else
+            hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW_CHUNK, THC, true>), g,
+                               dim3(64 * CO_NW_CHUNK), 0, h->stream, P, Q, h->dPart, slot, h->X, h->Y,
+                               h->TH, h->cgx, h->cgy, h->coKC, k);
         RS_HIP(hipGetLastError());
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
         if (!ctl) return RS_OK;
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
-        hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW, CTL>), g, b, 0, h->stream, Q,
-                           static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot, bmax,
-                           bidx, h->X, h->Y, h->TH, h->cgx);
+        if (whole)
+            hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW, THF, false, CTL>), g, dim3(64 * CO_NW), 0,
+                               h->stream, Q, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf,
+                               *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx, h->cgy, h->coKC);
+        else
+            hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW_CHUNK, THC, true, CTL>), g,
+                               dim3(64 * CO_NW_CHUNK), 0, h->stream, Q, static_cast<T*>(h->dP), h->dPart,
+                               h->nPart, filt, h->nf, *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx,
+                               h->cgy, h->coKC);
     } else if (h->streamed) {
         RS_TRY((pc_launch_stream<T, CTL>(h, P, Q, slot, bmax, bidx, ctl, prof_base)));
     } else if (h->tiling == 64 || h->tiling == 128) {
@@ -2140,10 +2201,35 @@ int pc_stream_scratch(int bx, int wr, int wc, size_t* bytes) {
 // The column kernels' limits: single-conditional wraps, the window in LDS, the
 // filter table in LDS.
 bool pc_cols_fit(const rs_pc* h) {
-    const int thmax = h->esz == 4 ? co_thmax<float>() : co_thmax<double>();
     const int vec = h->esz == 4 ? co_vec<float>() : co_vec<double>();
     return h->X >= CO_TX + 2 * HALF && h->Y >= CO_TY + 2 * HALF + 4 && h->Y % vec == 0 &&
-           h->TH >= CO_CH + 2 && h->TH <= thmax && h->nf <= RT_NFMAX;
+           h->TH >= CO_CH + 2 && h->nf <= RT_NFMAX;
+}
+
+// Theta chunking of the column form: kc = 0 picks it.  The whole extent in one
+// block per CU when it fits the LDS window (no halo layers); KC < TH puts KC + 6
+// layers in each of two blocks per CU.
+int pc_cols_set(rs_pc* h, int kc) {
+    const int thf = h->esz == 4 ? co_thmax<float>() : co_thmax<double>();
+    const int thc = h->esz == 4 ? co_thmax_chunk<float>() : co_thmax_chunk<double>();
+    if (kc <= 0) {
+        kc = h->TH;
+        if (h->TH > thf) {  // more layers than one block holds: the fewest chunks that fit
+            const int nch = (h->TH + thc - 2 * HALF - 1) / (thc - 2 * HALF);
+            kc = (h->TH + nch - 1) / nch;
+        }
+    }
+    RS_CHECK(kc >= 1 && kc <= h->TH, RS_ERR_ARG, "cols KC=%d outside [1, %d]", kc, h->TH);
+    RS_CHECK(kc < h->TH ? kc + 2 * HALF <= thc : h->TH <= thf, RS_ERR_ARG,
+             "cols KC=%d: %d window layers exceed the LDS window (%d whole, %d per chunk)", kc,
+             kc < h->TH ? kc + 2 * HALF : kc, thf, thc);
+    h->streamed = false;
+    h->cols = true;
+    h->cgx = (h->X + CO_TX - 1) / CO_TX;
+    h->cgy = (h->Y + CO_TY - 1) / CO_TY;
+    h->coKC = kc;
+    h->coNch = (h->TH + kc - 1) / kc;
+    return RS_OK;
 }
 
 int pc_choose_form(rs_pc* h) {
@@ -2159,17 +2245,13 @@ int pc_choose_form(rs_pc* h) {
         h->tiling = 0;
         return RS_OK;
     }
-    if (env && std::strcmp(env, "cols") == 0) {
+    if (env && (std::strcmp(env, "cols") == 0 || std::strncmp(env, "cols:", 5) == 0)) {
         RS_CHECK(pc_cols_fit(h), RS_ERR_ARG,
-                 "RS_PC_FORM=cols needs X >= %d, Y >= %d and a multiple of %d, %d <= TH <= %d and at "
-                 "most %d path filters",
+                 "RS_PC_FORM=cols needs X >= %d, Y >= %d and a multiple of %d, TH >= %d and at most %d "
+                 "path filters",
                  CO_TX + 2 * HALF, CO_TY + 2 * HALF + 4, h->esz == 4 ? co_vec<float>() : co_vec<double>(),
-                 CO_CH + 2, h->esz == 4 ? co_thmax<float>() : co_thmax<double>(), RT_NFMAX);
-        h->streamed = false;
-        h->cols = true;
-        h->cgx = (h->X + CO_TX - 1) / CO_TX;
-        h->cgy = (h->Y + CO_TY - 1) / CO_TY;
-        return RS_OK;
+                 CO_CH + 2, RT_NFMAX);
+        return pc_cols_set(h, env[4] == ':' ? std::atoi(env + 5) : 0);
     }
     const bool explicit_stream = env && std::strncmp(env, "stream:", 7) == 0;
     if (explicit_stream) {
@@ -2189,13 +2271,7 @@ int pc_choose_form(rs_pc* h) {
         }
         // large grids: the column form where it fits (128x128x72: 29.3 us per step
         // vs 38.8 us streamed, tools/pc_sweep.py), else the streamed form
-        if ((env == nullptr || env[0] == 0) && big && pc_cols_fit(h)) {
-            h->streamed = false;
-            h->cols = true;
-            h->cgx = (h->X + CO_TX - 1) / CO_TX;
-            h->cgy = (h->Y + CO_TY - 1) / CO_TY;
-            return RS_OK;
-        }
+        if ((env == nullptr || env[0] == 0) && big && pc_cols_fit(h)) return pc_cols_set(h, 0);
         bx = h->esz == 4 ? ST_DEF_BX : 1;
         wr = ST_DEF_WR;
         wc = ST_DEF_WC;
@@ -2284,7 +2360,7 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         return st;
     }
     if (h->cols) {
-        h->nPart = h->cgx * h->cgy;
+        h->nPart = h->cgx * h->cgy * h->coNch;
         h->nPathBlocks = h->nPart;
     } else if (h->streamed) {
         h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;

@@ -193,18 +193,24 @@ def test_simulate_driver(pcn):
 # tiled single-pass forms, the column form and the layer-streaming form at several tile shapes
 # (rows per wave, row groups, layers per block), incl. ragged tiles and grids
 # whose theta extent is not a multiple of the chunk
-FORMS = {'float32': ['rows', 'tiles', 'cols', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
+FORMS = {'float32': ['rows', 'tiles', 'cols', 'cols:5', 'cols:12', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:2,8,1,3',
                      'stream:1,4,2,3', 'stream:2,4,2,6'],
-         'float64': ['rows', 'tiles', 'cols', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
+         'float64': ['rows', 'tiles', 'cols', 'cols:7', 'stream:1,8,1,2', 'stream:1,8,1,5', 'stream:1,4,2,3']}
 
 
-def cols_fit(shape, precision):
-    """The column form's limits (posecell.hip pc_cols_fit): 16-byte row vectors
-    (Y a multiple of 4 cells at float32, 2 at float64), single-wrap halos, the
-    whole theta extent in LDS."""
+def cols_fit(shape, precision, form='cols'):
+    """The column form's limits (posecell.hip pc_cols_fit / pc_cols_set): 16-byte
+    row vectors (Y a multiple of 4 cells at float32, 2 at float64), single-wrap
+    halos, and the window layers in LDS (whole extent, or KC + 6 per chunk)."""
     X, Y, TH = shape
-    vec, thmax = (4, 76) if precision == 'float32' else (2, 42)
-    return X >= 14 and Y >= 18 and Y % vec == 0 and 10 <= TH <= thmax
+    vec, whole, chunk = (4, 76, 43) if precision == 'float32' else (2, 40, 21)
+    kc = int(form.split(':')[1]) if ':' in form else (TH if TH <= whole else 0)
+    if not (X >= 14 and Y >= 18 and Y % vec == 0 and TH >= 10):
+        return False
+    if kc == 0:
+        return True                     # chunked automatically
+    kc = min(kc, TH) if ':' not in form else kc
+    return kc <= TH and (kc + 6 <= chunk if kc < TH else TH <= whole)
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
@@ -218,12 +224,12 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
         want = ref.posecells
         for form in FORMS[precision]:
             monkeypatch.setenv('RS_PC_FORM', form)
-            if form == 'cols' and not cols_fit(shape, precision):
+            if form.startswith('cols') and not cols_fit(shape, precision, form):
                 with pytest.raises(ValueError):
                     pcn(shape, precision=precision)
                 continue
             net = pcn(shape, precision=precision)
-            assert net.step_form() == form.split(':')[0]
+            assert net.step_form() == form.split(':')[0], form
             net.inject(1, loc)
             got = net.run(od)
             assert [tuple(m) for m in got] == maxes, (shape, form)
@@ -236,7 +242,7 @@ def test_default_form_by_grid_size(pcn, monkeypatch):
     assert pcn((64, 64, 36)).step_form() == 'rows'
     assert pcn((128, 128, 72)).step_form() == 'cols'
     assert pcn((128, 130, 72)).step_form() == 'stream'    # Y not a multiple of 4: no cols
-    assert pcn((128, 128, 100)).step_form() == 'stream'   # theta extent beyond the LDS window
+    assert pcn((128, 128, 100)).step_form() == 'cols'     # theta extent beyond one block: chunked
     monkeypatch.setenv('RS_PC_FORM', 'stream:3,8,1')
     with pytest.raises(ValueError):
         pcn((64, 64, 36))

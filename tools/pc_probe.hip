@@ -128,11 +128,12 @@ int main(int argc, char** argv) {
         rs_pc_destroy(h);
         return 0;
     }
-    if (h->cols) {  // back-to-back launch costs of the column kernels
+    if (h->cols && h->coKC >= TH) {  // back-to-back launch costs of the column kernels
         hipEvent_t c0, c1;
         CK(hipEventCreate(&c0));
         CK(hipEventCreate(&c1));
         const dim3 g(h->cgx * h->cgy), b(64 * CO_NW);
+        constexpr int THF = co_thmax<float>();
         const int reps = 500;
         float t = 0;
         CK(hipEventRecord(c0, h->stream));
@@ -144,22 +145,27 @@ int main(int argc, char** argv) {
         const PcCtlRing ctl = make_ctl_ring(h, 0);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW>), g, b, 0, h->stream,
-                               (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->cgx, h->kf);
+            hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, THF, false>), g, b, 0, h->stream,
+                               (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->cgx,
+                               h->cgy, h->coKC, h->kf);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
         printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, PcCtlRing>), g, b, 0, h->stream,
+            hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, THF, false, PcCtlRing>), g, b, 0, h->stream,
                                (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
                                (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
-                               (unsigned*)nullptr, X, Y, TH, h->cgx);
+                               (unsigned*)nullptr, X, Y, TH, h->cgx, h->cgy, h->coKC);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
         printf("path alone: %.2f us/launch\n", 1e3 * t / reps);
+        rs_pc_destroy(h);
+        return 0;
+    }
+    if (h->cols) {
         rs_pc_destroy(h);
         return 0;
     }
