@@ -366,6 +366,50 @@ __device__ inline double block_sum_w(double v, double* s_red) {
     return t;
 }
 
+// Block barrier for LDS traffic only: waits for this wave's LDS operations, not
+// for its global stores (a __syncthreads fence would drain those too).
+__device__ inline void co_lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Wave-wide reductions by DPP row operations instead of ds_bpermute shuffles (six
+// dependent LDS round trips each): within every 16-lane row by quad_perm xor 1,
+// xor 2, row_half_mirror and row_mirror, then over the 4 rows by readlane.  Every
+// lane computes the same additions on the same two operands at each step, so the
+// result is identical in all lanes (wave-uniform) and deterministic.
+template <int CTRL>
+__device__ inline unsigned long long co_dpp64(unsigned long long v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
+__device__ inline unsigned long long co_readlane64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ inline double co_wave_sum(double v) {
+    v += __longlong_as_double((long long)co_dpp64<0xB1>((unsigned long long)__double_as_longlong(v)));
+    v += __longlong_as_double((long long)co_dpp64<0x4E>((unsigned long long)__double_as_longlong(v)));
+    v += __longlong_as_double((long long)co_dpp64<0x141>((unsigned long long)__double_as_longlong(v)));
+    v += __longlong_as_double((long long)co_dpp64<0x140>((unsigned long long)__double_as_longlong(v)));
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    return (__longlong_as_double((long long)co_readlane64(b, 0)) +
+            __longlong_as_double((long long)co_readlane64(b, 16))) +
+           (__longlong_as_double((long long)co_readlane64(b, 32)) +
+            __longlong_as_double((long long)co_readlane64(b, 48)));
+}
+__device__ inline unsigned long long co_wave_max(unsigned long long v) {
+    v = max(v, co_dpp64<0xB1>(v));
+    v = max(v, co_dpp64<0x4E>(v));
+    v = max(v, co_dpp64<0x141>(v));
+    v = max(v, co_dpp64<0x140>(v));
+    return max(max(co_readlane64(v, 0), co_readlane64(v, 16)),
+               max(co_readlane64(v, 32), co_readlane64(v, 48)));
+}
+
 template <typename T, int YP>
 __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P, T* __restrict__ Q,
                                                          double* __restrict__ part,
@@ -388,7 +432,7 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
         const int kk = tid / HX, a = tid - kk * HX;
         s_row[tid] = rs::wrapi(k0 - HALF + kk, TH) * X + rs::wrapi(i0 - HALF + a, X);
     }
-    __syncthreads();
+    co_lds_barrier();
 
     T v[RPW][JC];
 #pragma unroll
@@ -410,7 +454,7 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
             }
         }
     }
-    __syncthreads();
+    co_lds_barrier();
     PC_STAMP(0, 1);
 
     // y pass (7 taps along the row) then x pass (7 rows) in registers; one layer per wave
@@ -447,7 +491,7 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
             }
         }
     }
-    __syncthreads();
+    co_lds_barrier();
     PC_STAMP(0, 2);
 
     // theta pass + relu(v - inhib) (posecell_network.py:339-340) + partial sum; one row per wave
@@ -473,8 +517,15 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
             }
         }
     }
-    sum = block_sum_w<NW>(sum, s_red);
-    if (tid == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = sum;
+    sum = co_wave_sum(sum);
+    if (lane == 0) s_red[wave] = sum;
+    co_lds_barrier();  // the Q stores drain meanwhile
+    if (tid == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += s_red[w];
+        part[blockIdx.y * gridDim.x + blockIdx.x] = t;
+    }
     PC_STAMP(0, 3);
 }
 
@@ -490,7 +541,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     __shared__ T s_win[NR * RW];
     __shared__ T s_r[HK * BX * YP];
     __shared__ int s_row[NR];
-    __shared__ int s_L[HK], s_ox[HK], s_oy[HK], s_fi[HK];
+    __shared__ int s_oy[HK], s_fi[HK];
     __shared__ double s_red[NW];
     __shared__ T s_bv[NW];
     __shared__ unsigned s_bl[NW];
@@ -500,20 +551,19 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(1, 0);
 
+    // the block's control, and the row table straight from it (one barrier)
     if (tid < HK) {
         const int L = rs::wrapi(k0 - HALF + tid, TH);
-        s_L[tid] = L;
-        s_ox[tid] = rs::wrapi(ctl_ox(ctl, L), X);   // shifts may exceed the grid (vtrans large)
         s_oy[tid] = rs::wrapi(ctl_oy(ctl, L), Y);
         s_fi[tid] = ctl_fi(ctl, L);
     }
-    __syncthreads();
-    PC_STAMP(1, 1);
     if (tid < NR) {
-        const int kk = tid / HX, a = tid - kk * HX;
-        s_row[tid] = s_L[kk] * X + rs::wrapi(i0 - HALF + a + s_ox[kk], X);
+        const int kk = tid / HX, a = tid - kk * HX, L = rs::wrapi(k0 - HALF + kk, TH);
+        // shifts may exceed the grid (vtrans large)
+        s_row[tid] = L * X + rs::wrapi(i0 - HALF + a + rs::wrapi(ctl_ox(ctl, L), X), X);
     }
-    __syncthreads();
+    co_lds_barrier();
+    PC_STAMP(1, 1);
     PC_STAMP(1, 2);
 
     // shifted window rows: s_win[kk][a][HALF + d] = Q[L][(i0-3+a+ox) % X][(d + oy) % Y]
@@ -557,7 +607,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
             if (d >= Y - HALF) dst[d - (Y - HALF)] = v[q][jc];
         }
     }
-    __syncthreads();
+    co_lds_barrier();
     PC_STAMP(1, 3);
 
     // 7x7 per-layer correlation (:273-274), register-blocked over the BX rows, clamp (:300)
@@ -588,16 +638,25 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
             for (int i = 0; i < BX; ++i) s_r[(kk * BX + i) * YP + j] = acc[i] > T(0) ? acc[i] : T(0);
         }
     }
-    // normalisation total (its loads were issued at entry)
+    // normalisation total (its loads were issued at entry): per thread, then per
+    // wave by DPP, then over the waves through LDS behind the barrier that also
+    // publishes s_r
     double tot = pextra;
 #pragma unroll
     for (int u = 0; u < NPP; ++u) tot += pt[u];
-    tot = block_sum_w<NW>(tot, s_red);  // includes the barrier that publishes s_r
+    tot = co_wave_sum(tot);
+    if (lane == 0) s_red[wave] = tot;
+    co_lds_barrier();
+    tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) tot += s_red[w];
     PC_STAMP(1, 4);
 
-    // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319)
+    // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319):
+    // float32 as the largest packed (value, ~index) key, float64 as value/index pairs
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
+    unsigned long long bk = 0ull;
     {
         const T tt = (T)tot;
         const int kq = wave / BX, i = wave - kq * BX;
@@ -614,38 +673,47 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 if (tot != 0.0) val = val / tt;
                 P[((size_t)gk * X + gi) * Y + j] = val;
                 const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
-                if (val > bv || (val == bv && lin < bl)) {
+                if constexpr (sizeof(T) == 4) {
+                    bk = max(bk, argmax_key((float)val, lin));
+                } else if (val > bv || (val == bv && lin < bl)) {
                     bv = val;
                     bl = lin;
                 }
             }
         }
     }
-    // block argmax -> one (value, index) partial per block (pc_argmax_steps reduces)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const T ov = __shfl_xor(bv, off);
-        const unsigned ol = __shfl_xor(bl, off);
-        if (ov > bv || (ov == bv && ol < bl)) {
-            bv = ov;
-            bl = ol;
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    if constexpr (sizeof(T) == 4) {
+        __shared__ unsigned long long s_bk[NW];
+        bk = co_wave_max(bk);
+        if (lane == 0) s_bk[wave] = bk;
+        co_lds_barrier();
+        if (tid == 0) {
+            for (int w = 1; w < NW; ++w) bk = max(bk, s_bk[w]);
+            atomicMax(res_slot + (b & (RES_SLOTS - 1)), bk);
         }
-    }
-    if (lane == 0) {
-        s_bv[wave] = bv;
-        s_bl[wave] = bl;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        for (int w = 1; w < NW; ++w)
-            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
-                bv = s_bv[w];
-                bl = s_bl[w];
+    } else {
+        // block argmax -> one (value, index) partial per block (pc_argmax_steps reduces)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const T ov = __shfl_xor(bv, off);
+            const unsigned ol = __shfl_xor(bl, off);
+            if (ov > bv || (ov == bv && ol < bl)) {
+                bv = ov;
+                bl = ol;
             }
-        const int b = blockIdx.y * gridDim.x + blockIdx.x;
-        if constexpr (sizeof(T) == 4) {
-            atomicMax(res_slot + (b & (RES_SLOTS - 1)), argmax_key((float)bv, bl));
-        } else {
+        }
+        if (lane == 0) {
+            s_bv[wave] = bv;
+            s_bl[wave] = bl;
+        }
+        co_lds_barrier();
+        if (tid == 0) {
+            for (int w = 1; w < NW; ++w)
+                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                    bv = s_bv[w];
+                    bl = s_bl[w];
+                }
             bmax[b] = bv;
             bidx[b] = bl;
         }
@@ -1130,50 +1198,6 @@ constexpr int CO_LDS_CHUNK = 76 * 1024;   // two blocks per CU
 constexpr int CO_NW_CHUNK = 8;            // 16 waves per CU: the path kernel's VGPRs allow 4 per SIMD
 template <typename T>
 __host__ __device__ constexpr int co_thmax_chunk() { return CO_LDS_CHUNK / co_layer_bytes<T>(false); }
-
-// Block barrier for LDS traffic only: waits for this wave's LDS operations, not
-// for its global stores (a __syncthreads fence would drain those too).
-__device__ inline void co_lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// Wave-wide reductions by DPP row operations instead of ds_bpermute shuffles (six
-// dependent LDS round trips each): within every 16-lane row by quad_perm xor 1,
-// xor 2, row_half_mirror and row_mirror, then over the 4 rows by readlane.  Every
-// lane computes the same additions on the same two operands at each step, so the
-// result is identical in all lanes (wave-uniform) and deterministic.
-template <int CTRL>
-__device__ inline unsigned long long co_dpp64(unsigned long long v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, 0xF, 0xF, false);
-    return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
-__device__ inline unsigned long long co_readlane64(unsigned long long v, int l) {
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
-    return ((unsigned long long)hi << 32) | lo;
-}
-__device__ inline double co_wave_sum(double v) {
-    v += __longlong_as_double((long long)co_dpp64<0xB1>((unsigned long long)__double_as_longlong(v)));
-    v += __longlong_as_double((long long)co_dpp64<0x4E>((unsigned long long)__double_as_longlong(v)));
-    v += __longlong_as_double((long long)co_dpp64<0x141>((unsigned long long)__double_as_longlong(v)));
-    v += __longlong_as_double((long long)co_dpp64<0x140>((unsigned long long)__double_as_longlong(v)));
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    return (__longlong_as_double((long long)co_readlane64(b, 0)) +
-            __longlong_as_double((long long)co_readlane64(b, 16))) +
-           (__longlong_as_double((long long)co_readlane64(b, 32)) +
-            __longlong_as_double((long long)co_readlane64(b, 48)));
-}
-__device__ inline unsigned long long co_wave_max(unsigned long long v) {
-    v = max(v, co_dpp64<0xB1>(v));
-    v = max(v, co_dpp64<0x4E>(v));
-    v = max(v, co_dpp64<0x141>(v));
-    v = max(v, co_dpp64<0x140>(v));
-    return max(max(co_readlane64(v, 0), co_readlane64(v, 16)),
-               max(co_readlane64(v, 32), co_readlane64(v, 48)));
-}
 
 // window coordinate a in [-n, 2n) -> [0, n)
 __device__ inline int co_wrap(int a, int n) {
