@@ -351,7 +351,18 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
 // one memory round trip.  One halo layer per wave for the stencil passes, which
 // are register-blocked per column (a lane walks the x direction).
 // ---------------------------------------------------------------------------
-constexpr int RT_BX = 4, RT_BK = 2, RT_NT = 512, RT_NW = RT_NT / 64;
+// Row-tile shape: BK layers x BX rows per block, BK + 6 = BK * BX waves (one
+// window layer per wave in the y/x passes, one output row per wave in the theta
+// pass).  6 x 2 (12 waves) keeps the 64x64x36 grid at 192 blocks, one per CU:
+// 2 x 4 (8 waves) made 288 blocks, and the CUs that ran two of them set the
+// kernels' span (path 8.7 -> 5.2 us, excitation 4.6 -> 3.8 us first block start
+// to last block end; it also re-evaluates fewer halo rows and layers per output).
+// -D overrides for A/B builds of tools/pc_probe.hip.
+#ifndef PC_RT_BX
+#define PC_RT_BX 2
+#define PC_RT_BK 6
+#endif
+constexpr int RT_BX = PC_RT_BX, RT_BK = PC_RT_BK, RT_NW = RT_BK + 6, RT_NT = 64 * RT_NW;
 constexpr int RT_NFMAX = 8;  // filter tables up to this size are preloaded whole
 
 template <int NW>
