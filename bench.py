@@ -58,6 +58,9 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20, help='timed steps (template match calls)')
     ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--clock-warmup-ms', type=float, default=200.0,
+                    help='untimed matching before the warm-up steps of the headline leg, so the '
+                         'timed steps run at the GPU\'s steady clock (0 = off)')
     ap.add_argument('--batches-per-step', type=int, default=10,
                     help='query batches matched per step (one rs_vt_match_stream call)')
     ap.add_argument('--queries', type=int, default=1024, help='queries per batch (one scan launch)')
@@ -176,6 +179,18 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
             dev_ptr = bufs.offset(c * bpc * Q * queries[0].nbytes)
             return vts.match_stream((bpc, Q, dev_ptr)), c
         try:
+            # The GPU's clocks ramp up over the first tens of ms of load after idle
+            # (rocprof: the same scan launch 1,757 -> 1,499 us over its first 21
+            # launches, profiles/r2_v4_kernel_summary.md's trace): bring it to its
+            # steady clock with untimed steps before the W warm-up steps.
+            # Every rank runs the same number of them (each step may hold a collective).
+            if args.clock_warmup_ms > 0:
+                step(0)                               # sizes the stream's buffers
+                c0 = time.perf_counter()
+                step(1)
+                per = d.max(time.perf_counter() - c0)
+                for i in range(int(np.ceil(args.clock_warmup_ms * 1e-3 / max(per, 1e-4)))):
+                    step(i)
             for i in range(max(1, warmup)):          # the first sizes the stream's buffers
                 (sidx, _), c = step(i)
                 correct = correct and all(bool(np.all(sidx[b][srcs[c * bpc + b] >= 0] ==
@@ -192,9 +207,11 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
         bpc = 1
         for _ in range(warmup):
             match(staged=True)
-    # the timed steps run without the scan's timing events (two stream markers per
-    # batch); the scan kernel's duration comes from a separate timed pass
-    vts.set_timing(False)
+    # The scan kernel's duration is taken live in the timed steps: with timing on, a
+    # step's one scan launch (all bpc x Q queries of its HBM-resident batches) is
+    # bracketed by two HIP events on the stream it runs on.
+    vts.set_timing(True)
+    kernel_ms = []
     d.barrier()
     t0 = time.perf_counter()
     results = []
@@ -203,6 +220,7 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
             results.append(step(i))
         else:
             match(staged=True)
+        kernel_ms.append(vts.device_ms())
     t1 = time.perf_counter()
     d.barrier()
     dt = d.max(t1 - t0)
@@ -212,22 +230,8 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
                 s_ = srcs[c * bpc + b]
                 correct = correct and bool(np.all(sidx[b][s_ >= 0] == s_[s_ >= 0]))
         bufs.close()
-    vts.set_timing(True)
-    # the scan kernel's duration as the timed steps launch it: the stream scans all
-    # of a step's HBM-resident batches (bpc x Q queries) in one launch
-    kernel_ms = []
-    if pipeline == 'stream':
-        big = first_step
-        _lib.check(lib.rs_vt_match_batch(vts._h, len(big), _lib.ptr(big, ctypes.c_uint8),
-                                         _lib.RS_VT_FROZEN, None, None, None))
-        for _ in range(max(5, min(steps, 30))):
-            _lib.check(lib.rs_vt_match_batch(vts._h, len(big), None, _lib.RS_VT_FROZEN, None, None, None))
-            kernel_ms.append(vts.device_ms())
         match(staged=False)                  # stage one batch again for the PCIe-inclusive rate
-    else:
-        for _ in range(max(10, min(steps, 100))):
-            match(staged=True)
-            kernel_ms.append(vts.device_ms())
+    kernel_ms = [m for m in kernel_ms if m is not None and m >= 0]
     # PCIe-inclusive rate (queries uploaded from host memory every batch), not the value
     d.barrier()
     p0 = time.perf_counter()
@@ -245,8 +249,8 @@ def bench_templates(args, d, per_gpu=None, total=None, steps=None, warmup=None, 
         'timed_batches': steps * bpc,
         'timed_region_s': dt,
         'pcie_inclusive_value': compares * npcie / dtp,
-        'scan_ms': float(np.mean(kernel_ms)),
-        'scan_ms_min': float(np.min(kernel_ms)),
+        'scan_ms': float(np.mean(kernel_ms)) if kernel_ms else float('nan'),
+        'scan_ms_min': float(np.min(kernel_ms)) if kernel_ms else float('nan'),
         'kernel': SCAN_KERNELS.get(vts.scan_form(), vts.scan_form()),
         'compares_per_launch': float(len(range(d.rank, total, n))) * Q * bpc,
         'queries_per_launch': Q * bpc,
@@ -279,7 +283,7 @@ def scan_roofline(tv, tj, key):
     scan_s = tv['scan_ms'] * 1e-3
     roof = {'bound': 'valu', 'unit': 'G wave-instructions/s', 'peak': VALU_PEAK_GINSTS,
             'achieved': None, 'frac': None, 'traffic': None,
-            'kernel_ms': tv['scan_ms'], 'kernel_time_source': 'HIP events around each scan launch'}
+            'kernel_ms': tv['scan_ms'], 'kernel_time_source': 'HIP events around the scan launch of every timed step'}
     if same and rec.get('valu_insts_per_launch'):
         vi = rec['valu_insts_per_launch']
         roof['achieved'] = vi / scan_s / 1e9

@@ -228,8 +228,9 @@ int rs_vt_scores(rs_vt* h, int nq, const uint8_t* queries, int64_t t0, int64_t n
 int rs_vt_scan_local(rs_vt* h, int nq, const uint8_t* queries, uint64_t* local_keys);
 int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint64_t* best_score,
                   int64_t* best_index, uint8_t* is_new);
-/* device time (ms) of the scan kernel in the last match call (HIP events);
- * -1 when that scan ran untimed */
+/* device time (ms) of the scan kernel in the last match call (HIP events): for
+ * rs_vt_match_stream over HBM-resident batches, its one scan of all batches;
+ * -1 when that scan ran untimed or the call ran several scans */
 int rs_vt_last_ms(rs_vt* h, double* ms);
 /* HIP events around every scan (default on); off drops two stream markers per
  * match call (a ~5 us gap between the scan and the result export) */

@@ -1480,7 +1480,11 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
         h->dQsumRaw = h->dQsumStream;
         RS_TRY(vt_build_forms(h, (int)total, queries));
         const ScanOut out{h->dStream, nullptr, 0};
+        // the one scan of the call, bracketed by events when timing (rs_vt_last_ms)
+        if (h->timing) RS_HIP(hipEventRecord(h->ev0, h->stream));
         RS_TRY(vt_launch_scan<false>(h, false, lc, (int)total, out, h->rank, h->nranks));
+        if (h->timing) RS_HIP(hipEventRecord(h->ev1, h->stream));
+        h->timedScan = h->timing;
         if (h->comm) {
             ncclResult_t r = ncclAllReduce(h->dStream, h->dStream, total, ncclUint64, ncclMin, h->comm,
                                            h->stream);
@@ -1516,6 +1520,8 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     RS_HIP(hipMemcpyAsync(h->hStream, h->dStream, sizeof(unsigned long long) * total,
                           hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    if (!allplanes) h->timedScan = false;  // several scans: no single duration
+    else if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     for (size_t i = 0; i < total; ++i) {
         const unsigned long long k = h->hStream[i];
         if (best_index) best_index[i] = k == NO_KEY ? -1 : (int64_t)(k & 0xFFFFFFFFull);
