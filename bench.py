@@ -279,7 +279,9 @@ def scan_roofline(tv, tj, key):
     rec = (tj.get('scans') or {}).get(key) or {}
     same = (rec.get('templates_per_launch') == tv['templates_per_launch']
             and rec.get('queries') == tv['queries_per_launch']
-            and rec.get('kernel', '').startswith(tv['kernel']))
+            # the 64x32-template instantiation the bench launches (the profile's
+            # clock warm-up runs another one, vt_scan_plane_kernel<32, ...>)
+            and rec.get('kernel', '').startswith(tv['kernel'] + '<64'))
     scan_s = tv['scan_ms'] * 1e-3
     roof = {'bound': 'valu', 'unit': 'G wave-instructions/s', 'peak': VALU_PEAK_GINSTS,
             'achieved': None, 'frac': None, 'traffic': None,

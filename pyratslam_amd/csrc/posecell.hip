@@ -1179,6 +1179,9 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #ifndef PC_CO_FCOLS
 #define PC_CO_FCOLS 2   // 7x7 filter: output columns per task
 #endif
+#ifndef PC_CO_YREG
+#define PC_CO_YREG 1    // excitation y pass straight from the window loads (no LDS window)
+#endif
 // 9 waves: TH*TY = 576 x-pass tasks at TH = 72 (-D overrides for A/B builds of the probe)
 constexpr int CO_TX = PC_CO_TX, CO_TY = 8, CO_NW = PC_CO_NW;
 constexpr int CO_CH = 8;                        // layers per theta-pass task
@@ -1339,11 +1342,12 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
                                                           SepKernel<T> k) {
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
     constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, false>();
-    constexpr int LAYOUT = CHUNK ? CO_SWIZZLED : CO_PADDED, RP = (NCP + (CHUNK ? 0 : 1)) * VEC, WN = HX * RP;
+    [[maybe_unused]] constexpr int LAYOUT = CHUNK ? CO_SWIZZLED : CO_PADDED;
+    constexpr int RP = (NCP + (CHUNK ? 0 : 1)) * VEC, WN = HX * RP;
     constexpr int D = (VEC - HALF % VEC) % VEC;  // window column 0 within its row's first vector
     static_assert(2 * TX * TY <= WN, "x-pass outputs alias the window");
     static_assert(TY % VEC == 0 && D + HY <= NCP * VEC, "window row layout");
-    __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] window; then the x-pass outputs
+    __shared__ __attribute__((aligned(16))) T s_in[PC_CO_YREG ? 2 * THM * TX * TY : THM * WN];  // [L][r][RP] window; then the x-pass outputs
     __shared__ T s_ye[THM * HX * TY];
     __shared__ T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
@@ -1355,6 +1359,50 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
         res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
     PC_STAMP(5, 0);
+#if PC_CO_YREG
+    // y pass straight from the loads: task (L, r) = one window row per thread, its
+    // NCP 16-byte vectors loaded into registers (every row of the block in flight
+    // at once), TY outputs of both Gaussians into LDS; the window never visits LDS
+    {
+        constexpr int NR = (THM * HX + NT - 1) / NT;
+        const int nrow = ly.nl * HX;
+        V w[NR][NCP];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            const int t = min(tid + u * NT, nrow - 1), L = t / HX, r = t - L * HX;
+            const T* row = P + (size_t)ly.global(L, TH) * X * Y + (size_t)co_wrap(x0 - HALF + r, X) * Y;
+            const int c0 = co_wrap(y0 - HALF, Y) & ~(VEC - 1);
+#pragma unroll
+            for (int j = 0; j < NCP; ++j) w[u][j] = *reinterpret_cast<const V*>(row + co_wrap(c0 + j * VEC, Y));
+        }
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            const int t = tid + u * NT;
+            if (t >= nrow) break;
+            T v[NCP * VEC];
+#pragma unroll
+            for (int j = 0; j < NCP; ++j) {
+                if constexpr (VEC == 4) {
+                    v[4 * j] = w[u][j].x; v[4 * j + 1] = w[u][j].y; v[4 * j + 2] = w[u][j].z; v[4 * j + 3] = w[u][j].w;
+                } else {
+                    v[2 * j] = w[u][j].x; v[2 * j + 1] = w[u][j].y;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < TY; ++c) {
+                T e = 0, g = 0;
+#pragma unroll
+                for (int q = 0; q < FL; ++q) {
+                    e += k.ge[q] * v[D + c + q];
+                    g += k.gi[q] * v[D + c + q];
+                }
+                s_ye[t * TY + c] = e;
+                s_yi[t * TY + c] = g;
+            }
+        }
+    }
+    PC_STAMP(5, 1);
+#else
     co_load_window<T, NT, HX, NCP, THM, false, LAYOUT>(P, s_in, X, Y, TH, ly, x0, y0, nullptr, nullptr);
     co_lds_barrier();
     PC_STAMP(5, 1);
@@ -1383,6 +1431,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             s_yi[t * TY + c] = g;
         }
     }
+#endif
     co_lds_barrier();
     PC_STAMP(5, 2);
     // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows

@@ -921,7 +921,9 @@ struct rs_vt {
     size_t qpStreamCap = 0;                  // queries
     unsigned long long* dStream = nullptr;   // keys of rs_vt_match_stream, one row per batch
     unsigned long long* hStream = nullptr;   // pinned copy (nb * nq)
+    unsigned long long* hStreamDev = nullptr;  // hStream in the device's address space
     size_t streamCap = 0;
+    bool streamClean = false;                // dStream holds UINT64_MAX (vt_keys_export resets it)
     int bestClean = 0;     // leading dBest entries known to hold UINT64_MAX
     int bestPending = 0;   // bestClean once the keys of the running scan are exported
     // index lists for stores
@@ -1431,14 +1433,17 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(vt_grow_queries(h, nq));
     const size_t total = (size_t)nb * nq;
+    RS_CHECK(total <= INT32_MAX, RS_ERR_ARG, "too many queries in one stream");
     if (total > h->streamCap) {
         if (h->hStream) RS_HIP(hipHostFree(h->hStream));
         if (h->dStream) RS_HIP(hipFree(h->dStream));
         h->hStream = h->dStream = nullptr;
         h->streamCap = 0;
         RS_HIP(hipHostMalloc(&h->hStream, sizeof(unsigned long long) * total, hipHostMallocDefault));
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hStreamDev), h->hStream, 0));
         RS_HIP(hipMalloc(&h->dStream, sizeof(unsigned long long) * total));
         h->streamCap = total;
+        h->streamClean = false;
     }
     hipPointerAttribute_t attr{};
     const bool on_device = hipPointerGetAttributes(&attr, queries) == hipSuccess &&
@@ -1447,7 +1452,11 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
     RS_CHECK(!on_device || reinterpret_cast<uintptr_t>(queries) % 8 == 0, RS_ERR_ARG,
              "device-resident queries must be 8-byte aligned");
     const size_t qb = (size_t)h->H * h->W * nq;
-    RS_HIP(hipMemsetAsync(h->dStream, 0xFF, sizeof(unsigned long long) * total, h->stream));
+    // the keys start at UINT64_MAX: the export of the previous call reset them
+    // (one memset after allocation, or after a call that did not reach its export)
+    if (!h->streamClean)
+        RS_HIP(hipMemsetAsync(h->dStream, 0xFF, sizeof(unsigned long long) * h->streamCap, h->stream));
+    h->streamClean = false;
     h->stagedQ = 0;  // the forms no longer match dQraw
     h->timedScan = false;
     const int64_t lc = local_count_of(h, h->count);
@@ -1517,9 +1526,13 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
         RS_HIP(hipEventRecord(h->evComm, h->cstream));
         RS_HIP(hipStreamWaitEvent(h->stream, h->evComm, 0));
     }
-    RS_HIP(hipMemcpyAsync(h->hStream, h->dStream, sizeof(unsigned long long) * total,
-                          hipMemcpyDeviceToHost, h->stream));
+    // keys -> pinned host memory and reset for the next call, in one queued launch
+    // (in place of a device-to-host blit and a memset)
+    hipLaunchKernelGGL(vt_keys_export, dim3(std::min<size_t>((total + 255) / 256, 256)), dim3(256), 0,
+                       h->stream, h->dStream, (int)total, h->hStreamDev);
+    RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
+    h->streamClean = true;
     if (!allplanes) h->timedScan = false;  // several scans: no single duration
     else if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     for (size_t i = 0; i < total; ++i) {

@@ -1,5 +1,8 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_view_templates_gpu.py tests/test_configs_gpu.py > gpurun_out/vt_t.log 2>&1 || { echo "tests failed $?"; tail -5 gpurun_out/vt_t.log; exit 1; }
-tail -1 gpurun_out/vt_t.log
-timeout -k 10 600 python -u bench.py > gpurun_out/bench_r2i.json 2> gpurun_out/bench_r2i.err || exit 1
-timeout -k 10 600 python -u bench.py > gpurun_out/bench_r2j.json 2> gpurun_out/bench_r2j.err || exit 1
+fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 60 tools/pc_probe 128 128 72 > gpurun_out/probe128.log 2>&1
+rc=$?; cat gpurun_out/probe128.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/gpu_tests.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err
+rc=$?; tail -c 300 gpurun_out/bench.log; exit $rc

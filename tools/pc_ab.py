@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""A/B timing of the pose-cell step across library builds (GPU box).
+
+usage: python tools/pc_ab.py LIB.so [LIB2.so ...] [--shape 128,128,72] [--steps 2000] [--rounds 3]
+Each library runs in its own process (ctypes loads one copy), interleaved over
+rounds so clock drift hits every build alike: batched run() steps/s after a clock
+warm-up, and the state after the same odometry, compared across builds.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(path, shape, steps, check, precision, out):
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    from pyratslam_amd import _lib, synthetic
+    _lib.load(path)
+    from pyratslam_amd import PoseCellNetwork
+    od = synthetic.odometry(steps + check + 50, seed=0)
+    net = PoseCellNetwork(shape, precision=precision)
+    net.inject(1, tuple(s // 2 for s in shape))
+    mx = net.run(od[:check])
+    np.save(out, net.posecells)
+    t_end = time.perf_counter() + 0.3          # clock warm-up
+    while time.perf_counter() < t_end:
+        net.run(od[check:check + 50])
+    t0 = time.perf_counter()
+    net.run(od[check + 50:check + 50 + steps])
+    dt = time.perf_counter() - t0
+    print(json.dumps({'lib': path, 'form': net.step_form(), 'us_per_step': 1e6 * dt / steps,
+                      'argmax': [list(map(int, m)) for m in mx[-3:]]}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('libs', nargs='+')
+    ap.add_argument('--shape', default='128,128,72')
+    ap.add_argument('--steps', type=int, default=2000)
+    ap.add_argument('--check', type=int, default=40)
+    ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--precision', default='float32')
+    ap.add_argument('--child', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--out', default='')
+    a = ap.parse_args()
+    shape = tuple(int(s) for s in a.shape.split(','))
+    if a.child:
+        child(a.libs[0], shape, a.steps, a.check, a.precision, a.out)
+        return
+    import numpy as np
+    res = {lib: [] for lib in a.libs}
+    for rnd in range(a.rounds):
+        for i, lib in enumerate(a.libs):
+            out = '/tmp/pc_ab_%d.npy' % i
+            p = subprocess.run([sys.executable, __file__, lib, '--child', '--shape', a.shape, '--steps',
+                                str(a.steps), '--check', str(a.check), '--precision', a.precision,
+                                '--out', out], capture_output=True, text=True, timeout=300)
+            if p.returncode != 0:
+                print(p.stderr[-3000:], file=sys.stderr)
+                raise SystemExit(p.returncode)
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            res[lib].append(r['us_per_step'])
+            if rnd == 0:
+                s0, s = np.load('/tmp/pc_ab_0.npy'), np.load(out)
+                r['max_abs_diff_vs_first'] = float(np.abs(s - s0).max())
+                print(json.dumps(r), flush=True)
+    for lib in a.libs:
+        v = sorted(res[lib])
+        print(json.dumps({'lib': lib, 'us_per_step_min': v[0], 'us_per_step_median': v[len(v) // 2],
+                          'all': [round(x, 2) for x in res[lib]]}), flush=True)
+
+
+if __name__ == '__main__':
+    main()

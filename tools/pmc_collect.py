@@ -86,33 +86,27 @@ def summarise(base, c):
     return kernels
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--dir', required=True)
-    ap.add_argument('--tag', required=True)
-    ap.add_argument('--out', default='profiles')
-    a = ap.parse_args()
-    summary = {'tag': a.tag, 'method': __doc__.strip().splitlines()[2:11], 'configs': {}}
-    traffic = {'source': f'{a.tag}_pmc_summary.json', 'scans': {}, 'pose_cell': {}}
-    for c in list(SCANS) + list(PCS):
-        if not glob.glob(os.path.join(a.dir, c + '_*')):
-            continue
-        ks = summarise(a.dir, c)
-        summary['configs'][c] = ks
+def traffic_of(configs, tag):
+    """pmc_traffic.json (what bench.py reads) from the per-configuration kernels.
+    A scan configuration's profiled kernel is its 64x32-template instantiation
+    (vt_scan_plane_kernel<64, ...>): the 32x32 scans that warm the clocks first
+    run more, shorter dispatches and are not the configuration's kernel."""
+    traffic = {'source': f'{tag}_pmc_summary.json', 'scans': {}, 'pose_cell': {}}
+    for c, ks in configs.items():
         if c in SCANS:
-            scan = [k for k in ks if k.startswith('vt_scan') and ks[k].get('trace')]
+            scan = [k for k in ks if k.startswith('vt_scan') and '<64' in k and ks[k].get('trace')]
             if not scan:
                 continue
             k = max(scan, key=lambda n: ks[n]['trace']['calls'])
             e = ks[k]
-            traffic['scans'][{'headline': 'headline', 'stress': 'stress', 'library': 'library'}[c]] = {
+            traffic['scans'][c] = {
                 'kernel': k, 'templates_per_launch': SCANS[c][0], 'queries': SCANS[c][1],
                 'kernel_us_rocprof': e['trace']['avg_us'],
                 'valu_insts_per_launch': e.get('sq', {}).get('SQ_INSTS_VALU'),
                 'hbm_bytes_per_launch': e.get('hbm_bytes_per_dispatch'),
                 'wave_cycle_split': e.get('wave_cycle_split'),
-                'source': f'{a.tag}_pmc_summary.json'}
-        else:
+                'source': f'{tag}_pmc_summary.json'}
+        elif c in PCS:
             form, shape = PCS[c]
             ex = [k for k in ks if k.startswith('pc_excite') and ks[k].get('trace')]
             pa = [k for k in ks if k.startswith('pc_path') and ks[k].get('trace')]
@@ -125,7 +119,29 @@ def main():
                 'shape': shape, 'kernels': [ex, pa],
                 'kernel_us_rocprof': {'excite': ks[ex]['trace']['avg_us'], 'path': ks[pa]['trace']['avg_us']},
                 'hbm_bytes_per_step': sum(hb) if all(hb) else None,
-                'source': f'{a.tag}_pmc_summary.json'}
+                'source': f'{tag}_pmc_summary.json'}
+    return traffic
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--dir', default='')
+    ap.add_argument('--resummarise', action='store_true',
+                    help='rewrite pmc_traffic.json from profiles/<tag>_pmc_summary.json')
+    ap.add_argument('--tag', required=True)
+    ap.add_argument('--out', default='profiles')
+    a = ap.parse_args()
+    summary = {'tag': a.tag, 'method': __doc__.strip().splitlines()[2:11], 'configs': {}}
+    if a.resummarise:  # rebuild pmc_traffic.json from an existing summary (no raw data)
+        summary = json.load(open(os.path.join(a.out, f'{a.tag}_pmc_summary.json')))
+        with open(os.path.join(a.out, 'pmc_traffic.json'), 'w') as fh:
+            json.dump(traffic_of(summary['configs'], a.tag), fh, indent=1)
+        return
+    for c in list(SCANS) + list(PCS):
+        if not glob.glob(os.path.join(a.dir, c + '_*')):
+            continue
+        summary['configs'][c] = summarise(a.dir, c)
+    traffic = traffic_of(summary['configs'], a.tag)
     bench = trace_stats(os.path.join(a.dir, 'bench_trace'))
     if bench:
         summary['bench_command'] = {'command': 'python bench.py', 'kernels': bench}
