@@ -21,6 +21,7 @@
 //               reference's C order) via a packed 64-bit atomicMax.
 // max(conv(Q/t), 0) == max(conv(Q), 0)/t for t > 0, so the normalisation is
 // applied once, at the end of the step.
+#include <utility>
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -1179,6 +1180,21 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #ifndef PC_CO_FCOLS
 #define PC_CO_FCOLS 2   // 7x7 filter: output columns per task
 #endif
+#ifndef PC_CO_TVEC
+#define PC_CO_TVEC 0    // theta passes on 16-byte vectors: CO_TCL layers x VEC cells per task
+#endif
+#ifndef PC_CO_TCL
+#define PC_CO_TCL 2
+#endif
+#ifndef PC_CO_WT
+#define PC_CO_WT 0      // with PC_CO_TVEC: write-through (sc1) output stores
+#endif
+#ifndef PC_CO_PSPLIT
+#define PC_CO_PSPLIT 0  // path: window in two parts, the first part's layers filtered early
+#endif
+#ifndef PC_CO_FTLATE
+#define PC_CO_FTLATE 0  // path: filter table staged into LDS behind the window loads
+#endif
 #ifndef PC_CO_YREG
 #define PC_CO_YREG 1    // excitation y pass straight from the window loads (no LDS window)
 #endif
@@ -1219,12 +1235,34 @@ __device__ inline int co_wrap(int a, int n) {
     return a - (a >= n ? n : 0);
 }
 
+// A 16-byte output vector at element offset e of a volume of nbytes bytes:
+// PC_CO_WT stores it write-through (sc1: the line leaves the XCD's L2 at once, so
+// the kernel ends with nothing dirty to write back), else a plain store.
+template <typename T, typename V>
+__device__ inline void co_put(T* __restrict__ base, size_t e, V v, bool wt, int nbytes) {
+#if PC_CO_WT
+    if (wt) {
+        typedef unsigned v4u __attribute__((ext_vector_type(4)));
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, nbytes, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)(e * sizeof(T)), 0, 16);
+        return;
+    }
+#endif
+    (void)wt;
+    (void)nbytes;
+    *reinterpret_cast<V*>(base + e) = v;
+}
+
 template <typename T>
 struct CoVec;
+// native vector types: their copies are vector loads/stores, not memcpys (a window
+// array of HIP_vector_type kept live across a loop stayed in scratch)
+typedef float co_f4 __attribute__((ext_vector_type(4)));
+typedef double co_d2 __attribute__((ext_vector_type(2)));
 template <>
-struct CoVec<float> { using type = float4; };
+struct CoVec<float> { using type = co_f4; };
 template <>
-struct CoVec<double> { using type = double2; };
+struct CoVec<double> { using type = co_d2; };
 
 
 // Layers of one column block: nl = nout + 2*halo window layers, local layer L
@@ -1237,6 +1275,10 @@ struct CoLayers {
     // local layer of theta tap a (0..13) for the outputs of chunk j (8 per task)
     __device__ inline int tap(int j, int a, int TH) const {
         return CHUNK ? min(j * 8 + a, nl - 1) : co_wrap(j * 8 - HALF + a, TH);
+    }
+    // the same for chunks of cl output layers
+    __device__ inline int tapc(int j, int a, int cl, int TH) const {
+        return CHUNK ? min(j * cl + a, nl - 1) : co_wrap(j * cl - HALF + a, TH);
     }
 };
 
@@ -1279,7 +1321,7 @@ struct CoPart {
     }
 };
 
-template <typename T, int NT, int HX, int NCP, bool SHIFTED, bool CHUNK, typename PT, typename V, int LPT>
+template <typename T, int NT, int HX, int NCP, bool SHIFTED, bool CHUNK, typename PT, int U0 = 0, typename V, int LPT>
 __device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, int Y, int TH,
                                 const CoLayers<CHUNK>& ly, int x0, int y0, const int* s_ox, const int* s_oy) {
     constexpr int VEC = co_vec<T>();
@@ -1288,7 +1330,7 @@ __device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, i
 #pragma clang loop unroll(full)
     for (int u = 0; u < LPT; ++u) {
         int L, r, j;
-        PT::at(min(tid + u * NT, n - 1), L, r, j);
+        PT::at(min(tid + (U0 + u) * NT, n - 1), L, r, j);
         int gr = co_wrap(x0 - HALF + r, X), gc = co_wrap(y0 - HALF, Y);
         if constexpr (SHIFTED) {
             gr += s_ox[L];
@@ -1308,16 +1350,25 @@ __device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, i
     }
 }
 
-template <int NT, int HX, int NCP, int LAYOUT, typename PT, bool CHUNK, typename T, typename V, int LPT>
-__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly) {
+template <int NT, int HX, int NCP, int LAYOUT, typename PT, int U0, bool CHUNK, typename T, typename V, int LPT,
+          int... U>
+__device__ inline void co_store_seq(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly,
+                                    std::integer_sequence<int, U...>) {
     const int n = ly.nl * PT::PER_LAYER, tid = threadIdx.x;
-#pragma clang loop unroll(full)
-    for (int u = 0; u < LPT; ++u) {
-        const int e = tid + u * NT;
+    auto one = [&](auto uc) __attribute__((always_inline)) {
+        constexpr int u = decltype(uc)::value;
+        const int e = tid + (U0 + u) * NT;
         int L, r, j;
         PT::at(e < n ? e : n - 1, L, r, j);
         if (e < n) reinterpret_cast<V*>(s_in)[co_slot<NCP, LAYOUT>(L * HX + r, j)] = w[u];
-    }
+    };
+    (one(std::integral_constant<int, U>{}), ...);
+}
+// (an index sequence, not a loop: constant indices into w even where the unroller
+// gives up, so w stays in registers)
+template <int NT, int HX, int NCP, int LAYOUT, typename PT, int U0 = 0, bool CHUNK, typename T, typename V, int LPT>
+__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly) {
+    co_store_seq<NT, HX, NCP, LAYOUT, PT, U0>(w, s_in, ly, std::make_integer_sequence<int, LPT>{});
 }
 
 // The whole window of a block into LDS, every load in flight together.
@@ -1459,6 +1510,51 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     }
     co_lds_barrier();
     PC_STAMP(5, 3);
+#if PC_CO_TVEC
+    // theta pass: task (row i, column vector cv, chunk j) -> CO_TCL output layers of
+    // VEC cells from CO_TCL + 6 x-pass layers read as 16-byte vectors; each output
+    // layer leaves as one 16-byte store
+    double sum = 0.0;
+    {
+        constexpr int CL = PC_CO_TCL, NCV = TY / VEC;
+        const int ncl = (ly.nout + CL - 1) / CL;
+        const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
+        const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
+        for (int t = tid; t < TX * NCV * ncl; t += NT) {
+            const int j = t / (TX * NCV), rem = t - j * (TX * NCV), i = rem / NCV, cv = rem - i * NCV;
+            const int gi = x0 + i, gy = y0 + cv * VEC;
+            V xe[CL + 2 * HALF], xi[CL + 2 * HALF];
+#pragma unroll
+            for (int a = 0; a < CL + 2 * HALF; ++a) {
+                const int L = ly.tapc(j, a, CL, TH);
+                xe[a] = *reinterpret_cast<const V*>(s_xe + (L * TX + i) * TY + cv * VEC);
+                xi[a] = *reinterpret_cast<const V*>(s_xi + (L * TX + i) * TY + cv * VEC);
+            }
+            const bool mine = gi < X && gy < Y;
+#pragma unroll
+            for (int o = 0; o < CL; ++o) {
+                const int lo = j * CL + o, gk = ly.k0 + lo;
+                V e = 0, g = 0;
+#pragma unroll
+                for (int q = 0; q < FL; ++q) {
+                    e += k.ge[q] * xe[o + q];
+                    g += k.gi[q] * xi[o + q];
+                }
+                const V v = (e - g) * k.scale;
+                V qv;
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) qv[c] = (v[c] < k.inhib) ? T(0) : v[c] - k.inhib;
+                if (mine && lo < ly.nout) {
+#ifndef PC_DIAG_NOSTORE
+                    co_put(Q, ((size_t)gk * X + gi) * Y + gy, qv, wt, nbytes);
+#endif
+#pragma unroll
+                    for (int c = 0; c < VEC; ++c) sum += (double)qv[c];
+                }
+            }
+        }
+    }
+#else
     // theta pass: task (cell p, chunk j) -> CO_CH output layers of one cell from
     // CO_CH + 6 x-pass layers (lanes <-> cells: a wave reads 64 consecutive LDS words)
     double sum = 0.0;
@@ -1493,6 +1589,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             }
         }
     }
+#endif
     sum = co_wave_sum(sum);
     if ((tid & 63) == 0) s_red[tid >> 6] = sum;
     co_lds_barrier();  // the Q stores drain meanwhile
@@ -1544,10 +1641,19 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         // window row (L, r) starts this many cells into its first vector
         s_yd[L] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
     }
+#if PC_CO_FTLATE
+    // the filter table's loads are issued now and land in LDS behind the window's
+    // (the first barrier waits for the shifts alone)
+    constexpr int NFR = (RT_NFMAX * FT + NT - 1) / NT;
+    T fr[NFR];
+#pragma unroll
+    for (int u = 0; u < NFR; ++u) fr[u] = tid + u * NT < nf * FT ? filt[tid + u * NT] : T(0);
+#else
     for (int i = tid; i < nf * FT; i += NT) {
         const int fi = i / FT;
         s_ftab[fi * ST_FTP + (i - fi * FT)] = filt[i];
     }
+#endif
     T zf[FL];
 #pragma unroll
     for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
@@ -1556,8 +1662,14 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // window (L, r, c) <-> Q[L][(x0-3+r+ox[L]) % X][(y0-3+c+oy[L]) % Y], at LDS column
     // c + d[L] of row (L, r), d[L] = (y0 - 3 + oy[L]) % Y % VEC
     using P0 = CoPart<HX, NCP>;
-    typename CoVec<T>::type win[(THM * P0::PER_LAYER + NT - 1) / NT];
+    constexpr int LPT = (THM * P0::PER_LAYER + NT - 1) / NT;
+    // PC_CO_PSPLIT: the window lands in two parts (loads u < UA, then the rest; vmcnt
+    // waits retire in issue order), and the layers complete in the first part are
+    // filtered while the second part's loads are still in flight
+    constexpr int UA = PC_CO_PSPLIT ? (LPT + 1) / 2 : LPT, UB = LPT - UA > 0 ? LPT - UA : 1;
+    typename CoVec<T>::type win[UA], win2[UB];
     co_issue<T, NT, HX, NCP, true, CHUNK, P0>(win, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
+    if constexpr (UA < LPT) co_issue<T, NT, HX, NCP, true, CHUNK, P0, UA>(win2, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < NPL; ++u) tot += pt[u];
@@ -1565,6 +1677,13 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     tot = co_wave_sum(tot);
     const T tt = (T)tot;
     co_store<NT, HX, NCP, CO_PLAIN, P0>(win, s_in, ly);
+#if PC_CO_FTLATE
+#pragma unroll
+    for (int u = 0; u < NFR; ++u) {
+        const int i = tid + u * NT, fi = i / FT;
+        if (i < nf * FT) s_ftab[fi * ST_FTP + (i - fi * FT)] = fr[u];
+    }
+#endif
     co_lds_barrier();
     PC_STAMP(6, 2);
     // 7x7 filter: task (L, column group, row part) -> TX/FS rows x CP columns of
@@ -1573,37 +1692,46 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // of them spills at 3 waves per SIMD)
     constexpr int FS = PC_CO_FSPLIT, TXH = TX / FS, CP = PC_CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    for (int t = tid; t < ly.nl * NCG * FS; t += NT) {
-        const int L = t / (FS * NCG), rem = t - L * FS * NCG, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
-        T f[FT];
-        st_filter<T>(s_ftab + s_fo[L], f);
-        T acc[TXH][CP];
+    const int LA = UA < LPT ? min(ly.nl, (UA * NT) / P0::PER_LAYER) : ly.nl;
+    auto filter = [&](int t0, int t1) __attribute__((always_inline)) {
+        for (int t = tid + t0; t < t1; t += NT) {
+            const int L = t / (FS * NCG), rem = t - L * FS * NCG, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
+            T f[FT];
+            st_filter<T>(s_ftab + s_fo[L], f);
+            T acc[TXH][CP];
 #pragma unroll
-        for (int i = 0; i < TXH; ++i)
+            for (int i = 0; i < TXH; ++i)
 #pragma unroll
-            for (int c = 0; c < CP; ++c) acc[i][c] = 0;
-        const T* win = s_in + L * WN + hf * TXH * RP + s_yd[L] + c0;
+                for (int c = 0; c < CP; ++c) acc[i][c] = 0;
+            const T* win = s_in + L * WN + hf * TXH * RP + s_yd[L] + c0;
 #pragma unroll
-        for (int a = 0; a < TXH + 2 * HALF; ++a) {
-            T w[FL + CP - 1];
+            for (int a = 0; a < TXH + 2 * HALF; ++a) {
+                T w[FL + CP - 1];
 #pragma unroll
-            for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[a * RP + q];
-            if (a % PC_CO_FROWS == PC_CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[a * RP + q];
+                if (a % PC_CO_FROWS == PC_CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < TXH; ++i) {
-                const int x = a - i;
-                if (x < 0 || x >= FL) continue;
+                for (int i = 0; i < TXH; ++i) {
+                    const int x = a - i;
+                    if (x < 0 || x >= FL) continue;
+#pragma unroll
+                    for (int c = 0; c < CP; ++c)
+#pragma unroll
+                        for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < TXH; ++i)
 #pragma unroll
                 for (int c = 0; c < CP; ++c)
-#pragma unroll
-                    for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
-            }
+                    s_p[(L * TX + hf * TXH + i) * TY + c0 + c] = acc[i][c] > T(0) ? acc[i][c] : T(0);
         }
-#pragma unroll
-        for (int i = 0; i < TXH; ++i)
-#pragma unroll
-            for (int c = 0; c < CP; ++c)
-                s_p[(L * TX + hf * TXH + i) * TY + c0 + c] = acc[i][c] > T(0) ? acc[i][c] : T(0);
+    };
+    filter(0, LA * NCG * FS);
+    if constexpr (UA < LPT) {
+        co_store<NT, HX, NCP, CO_PLAIN, P0, UA>(win2, s_in, ly);
+        co_lds_barrier();
+        filter(LA * NCG * FS, ly.nl * NCG * FS);
     }
     co_lds_barrier();
     PC_STAMP(6, 3);
@@ -1613,6 +1741,54 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
+#if PC_CO_TVEC
+    {
+        // task (row i, column vector cv, chunk j): CO_TCL output layers of VEC cells
+        // from 16-byte LDS vectors, one 16-byte store per output layer
+        using V = typename CoVec<T>::type;
+        constexpr int CL = PC_CO_TCL, NCV = TY / VEC;
+        const int ncl = (ly.nout + CL - 1) / CL;
+        const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
+        const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
+        for (int t = tid; t < TX * NCV * ncl; t += NT) {
+            const int j = t / (TX * NCV), rem = t - j * (TX * NCV), i = rem / NCV, cv = rem - i * NCV;
+            const int gi = x0 + i, gy = y0 + cv * VEC;
+            V r[CL + 2 * HALF];
+#pragma unroll
+            for (int a = 0; a < CL + 2 * HALF; ++a)
+                r[a] = *reinterpret_cast<const V*>(s_p + (ly.tapc(j, a, CL, TH) * TX + i) * TY + cv * VEC);
+            const bool mine = gi < X && gy < Y;
+#pragma unroll
+            for (int o = 0; o < CL; ++o) {
+                const int lo = j * CL + o, gk = ly.k0 + lo;
+                V v = 0;
+#pragma unroll
+                for (int z = 0; z < FL; ++z) v += r[o + z] * zf[z];
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) {
+                    T x = v[c] > T(0) ? v[c] : T(0);
+                    if (tot != 0.0) x = x / tt;
+                    v[c] = x;
+                }
+                if (mine && lo < ly.nout) {
+#ifndef PC_DIAG_NOSTORE
+                    co_put(P, ((size_t)gk * X + gi) * Y + gy, v, wt, nbytes);
+#endif
+#pragma unroll
+                    for (int c = 0; c < VEC; ++c) {
+                        const unsigned lin = ((unsigned)gi * Y + gy + c) * TH + gk;
+                        if constexpr (sizeof(T) == 4) {
+                            bk = max(bk, argmax_key((float)v[c], lin));
+                        } else if (v[c] > bv || (v[c] == bv && lin < bl)) {
+                            bv = v[c];
+                            bl = lin;
+                        }
+                    }
+                }
+            }
+        }
+    }
+#else
     const int nch = (ly.nout + CO_CH - 1) / CO_CH;
     for (int t = tid; t < TX * TY * nch; t += NT) {
         const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
@@ -1643,6 +1819,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
             }
         }
     }
+#endif
     if constexpr (sizeof(T) == 4) {
         __shared__ unsigned long long s_bk[NW];
         bk = co_wave_max(bk);
@@ -2143,7 +2320,11 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
     RS_TRY(pc_grow_steps(h, n));
-    const bool inline_ctl = n == 1 && h->TH <= CTL_INLINE_MAX;
+    static const bool force_inline = [] {  // A/B: per-step control as kernel arguments in batches too
+        const char* e = std::getenv("RS_PC_CTL");
+        return e && std::strcmp(e, "inline") == 0;
+    }();
+    const bool inline_ctl = (n == 1 || force_inline) && h->TH <= CTL_INLINE_MAX;
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,

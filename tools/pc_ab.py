@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of the pose-cell step across library builds (GPU box).
 
-usage: python tools/pc_ab.py LIB.so [LIB2.so ...] [--shape 128,128,72] [--steps 2000] [--rounds 3]
+usage: python tools/pc_ab.py LIB.so[@ENV=V,...] [LIB2.so ...] [--shape 128,128,72] [--steps 2000] [--rounds 3]
+(``@RS_PC_CTL=inline`` runs that library with the variable set)
 Each library runs in its own process (ctypes loads one copy), interleaved over
 rounds so clock drift hits every build alike: batched run() steps/s after a clock
 warm-up, and the state after the same odometry, compared across builds.
@@ -57,13 +58,16 @@ def main():
     for rnd in range(a.rounds):
         for i, lib in enumerate(a.libs):
             out = '/tmp/pc_ab_%d.npy' % i
-            p = subprocess.run([sys.executable, __file__, lib, '--child', '--shape', a.shape, '--steps',
+            path, _, envs = lib.partition('@')
+            env = dict(os.environ, **dict(kv.split('=', 1) for kv in envs.split(',') if kv))
+            p = subprocess.run([sys.executable, __file__, path, '--child', '--shape', a.shape, '--steps',
                                 str(a.steps), '--check', str(a.check), '--precision', a.precision,
-                                '--out', out], capture_output=True, text=True, timeout=300)
+                                '--out', out], capture_output=True, text=True, timeout=300, env=env)
             if p.returncode != 0:
                 print(p.stderr[-3000:], file=sys.stderr)
                 raise SystemExit(p.returncode)
             r = json.loads(p.stdout.strip().splitlines()[-1])
+            r['lib'] = lib
             res[lib].append(r['us_per_step'])
             if rnd == 0:
                 s0, s = np.load('/tmp/pc_ab_0.npy'), np.load(out)

@@ -110,6 +110,22 @@ int main(int argc, char** argv) {
             printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph[i]) * 1e-3,
                    *std::max_element(ph[i].begin(), ph[i].end()) * 1e-3);
     }
+    // the last step's kernel boundary: excitation's last block end -> path's first block start
+    for (int ek = 0; ek < 7; ek += 5) {  // (0, 1) rows, (5, 6) cols
+        const int pk = ek + 1;
+        if (st[(size_t)ek * 4096 * 8] == 0 || st[(size_t)pk * 4096 * 8] == 0) continue;
+        unsigned long long e1 = 0, p0 = ~0ull, e0 = ~0ull, p1 = 0;
+        for (int b = 0; b < nb; ++b) {
+            const unsigned long long* re = &st[((size_t)ek * 4096 + b) * 8];
+            const unsigned long long* rp = &st[((size_t)pk * 4096 + b) * 8];
+            e0 = std::min(e0, re[0]);
+            e1 = std::max(e1, re[kns[ek] - 1]);
+            p0 = std::min(p0, rp[0]);
+            p1 = std::max(p1, rp[kns[pk] - 1]);
+        }
+        printf("boundary %s -> %s: %.2f us (excite first start -> path last end %.2f us)\n", kname[ek],
+               kname[pk], ((double)p0 - (double)e1) * 1e-2, ((double)p1 - (double)e0) * 1e-2);
+    }
     if (st[(size_t)4 * 4096 * 8] != 0) {  // shader-clock phases of layer 5 (excite stream)
         const char* nm[6] = {"vmcnt wait", "lds store+prefetch+barrier", "y pass", "barrier 2",
                              "x pass", "theta pass"};
