@@ -74,9 +74,12 @@ __device__ inline int ctl_oy(const PcCtlRing& c, int L) { return c.oy[L]; }
 __device__ inline int ctl_fi(const PcCtlRing& c, int L) { return c.f[L]; }
 __device__ inline double ctl_zf(const PcCtlRing& c, int z) { return c.zf[z]; }
 
-// float32 argmax: one packed key per block, max-reduced into 8 slots (spread so
-// no address sees more than nblocks/8 atomics); the host takes the max of 8.
-constexpr int RES_SLOTS = 8;
+// float32 argmax: one packed key per block, max-reduced into slot b % RES_SLOTS;
+// pc_res_export takes each step's max.  256 slots: one block per slot on the
+// column and rows grids (with 8 slots, 32 contending 64-bit atomics per address
+// held each step's end back: 64x64x36 13.35 -> 12.32 us per batched step,
+// 128x128x72 27.7 -> 26.8, tools/pc_ab.py).
+constexpr int RES_SLOTS = 256;
 __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
     return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
 }
@@ -145,9 +148,8 @@ __global__ __launch_bounds__(NT) void pc_excite_kernel(const T* __restrict__ P, 
 
     const int tid = threadIdx.x;
     const int j0 = blockIdx.x * BY, i0 = blockIdx.y * BX, k0 = blockIdx.z * BK;
-    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0 && blockIdx.y == 0 &&
-        blockIdx.z == 0)
-        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+    if (res_slot != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0)
+        for (int i = tid; i < RES_SLOTS; i += NT) res_slot[i] = 0ull;  // this step's path kernel max-reduces into them
 
     for (int idx = tid; idx < HK * HX * HY; idx += NT) {
         const int kk = idx / (HX * HY);
@@ -438,8 +440,8 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int i0 = blockIdx.x * BX, k0 = blockIdx.y * BK;
     PC_STAMP(0, 0);
-    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0 && blockIdx.y == 0)
-        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+    if (res_slot != nullptr && blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = tid; i < RES_SLOTS; i += blockDim.x) res_slot[i] = 0ull;  // this step's path kernel max-reduces into them
     if (tid < NR) {
         const int kk = tid / HX, a = tid - kk * HX;
         s_row[tid] = rs::wrapi(k0 - HALF + kk, TH) * X + rs::wrapi(i0 - HALF + a, X);
@@ -822,8 +824,8 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_excite_stream(con
     const int nL = min(G.KC, TH - k0) + 2 * HALF;
     const int gy = y0 + col;
     PC_STAMP(2, 0);
-    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
-        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+    if (res_slot != nullptr && blockIdx.x == 0)
+        for (int i = tid; i < RES_SLOTS; i += blockDim.x) res_slot[i] = 0ull;  // this step's path kernel max-reduces into them
 
     // window element e = (row r, col c) <-> P[L][(i0-3+r) % X][(y0-3+c) % Y]: the
     // in-layer offset is fixed over layers
@@ -1180,27 +1182,10 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #ifndef PC_CO_FCOLS
 #define PC_CO_FCOLS 2   // 7x7 filter: output columns per task
 #endif
-#ifndef PC_CO_TVEC
-#define PC_CO_TVEC 0    // theta passes on 16-byte vectors: CO_TCL layers x VEC cells per task
-#endif
-#ifndef PC_CO_TCL
-#define PC_CO_TCL 2
-#endif
-#ifndef PC_CO_WT
-#define PC_CO_WT 0      // with PC_CO_TVEC: write-through (sc1) output stores
-#endif
-#ifndef PC_CO_PSPLIT
-#define PC_CO_PSPLIT 0  // path: window in two parts, the first part's layers filtered early
-#endif
-#ifndef PC_CO_FTLATE
-#define PC_CO_FTLATE 0  // path: filter table staged into LDS behind the window loads
-#endif
-#ifndef PC_CO_YREG
-#define PC_CO_YREG 1    // excitation y pass straight from the window loads (no LDS window)
-#endif
 // 9 waves: TH*TY = 576 x-pass tasks at TH = 72 (-D overrides for A/B builds of the probe)
 constexpr int CO_TX = PC_CO_TX, CO_TY = 8, CO_NW = PC_CO_NW;
-constexpr int CO_CH = 8;                        // layers per theta-pass task
+constexpr int CO_CH = 8;                        // layers per theta-pass task (scalar stream/rows helpers)
+constexpr int CO_TCL = 2;                       // column theta passes: output layers per task
 constexpr int CO_LDS = 150 * 1024;              // LDS budget of the excitation kernel
 // Window rows are loaded as 16-byte vectors of VEC = 16 / sizeof(T) cells from a
 // VEC-aligned start (Y % VEC == 0, so a vector never straddles the wrap): a row of
@@ -1235,19 +1220,19 @@ __device__ inline int co_wrap(int a, int n) {
     return a - (a >= n ? n : 0);
 }
 
-// A 16-byte output vector at element offset e of a volume of nbytes bytes:
-// PC_CO_WT stores it write-through (sc1: the line leaves the XCD's L2 at once, so
-// the kernel ends with nothing dirty to write back), else a plain store.
+// A 16-byte output vector at element offset e of a volume of nbytes bytes, stored
+// write-through (sc1: the line leaves the XCD's L2 at once, so the kernel ends with
+// nothing dirty to write back -- 128x128x72: 27.7 -> 24.3 us per batched step with
+// the 16-byte theta-pass stores, tools/pc_ab.py; the excite -> path boundary gap
+// 3.5 -> 2.1 us, tools/pc_probe.hip); volumes of 2 GiB or more: plain stores.
 template <typename T, typename V>
 __device__ inline void co_put(T* __restrict__ base, size_t e, V v, bool wt, int nbytes) {
-#if PC_CO_WT
     if (wt) {
         typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, nbytes, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)(e * sizeof(T)), 0, 16);
         return;
     }
-#endif
     (void)wt;
     (void)nbytes;
     *reinterpret_cast<V*>(base + e) = v;
@@ -1398,7 +1383,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     constexpr int D = (VEC - HALF % VEC) % VEC;  // window column 0 within its row's first vector
     static_assert(2 * TX * TY <= WN, "x-pass outputs alias the window");
     static_assert(TY % VEC == 0 && D + HY <= NCP * VEC, "window row layout");
-    __shared__ __attribute__((aligned(16))) T s_in[PC_CO_YREG ? 2 * THM * TX * TY : THM * WN];  // [L][r][RP] window; then the x-pass outputs
+    __shared__ __attribute__((aligned(16))) T s_in[2 * THM * TX * TY];  // the x-pass outputs (e, i)
     __shared__ T s_ye[THM * HX * TY];
     __shared__ T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
@@ -1407,10 +1392,9 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     const int tile = st_tile(blockIdx.x, gridDim.x), xy = tile % (gx * gy);
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
-    if (res_slot != nullptr && tid < RES_SLOTS && blockIdx.x == 0)
-        res_slot[tid] = 0ull;  // this step's path kernel max-reduces into them
+    if (res_slot != nullptr && blockIdx.x == 0)
+        for (int i = tid; i < RES_SLOTS; i += blockDim.x) res_slot[i] = 0ull;  // this step's path kernel max-reduces into them
     PC_STAMP(5, 0);
-#if PC_CO_YREG
     // y pass straight from the loads: task (L, r) = one window row per thread, its
     // NCP 16-byte vectors loaded into registers (every row of the block in flight
     // at once), TY outputs of both Gaussians into LDS; the window never visits LDS
@@ -1453,36 +1437,6 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
         }
     }
     PC_STAMP(5, 1);
-#else
-    co_load_window<T, NT, HX, NCP, THM, false, LAYOUT>(P, s_in, X, Y, TH, ly, x0, y0, nullptr, nullptr);
-    co_lds_barrier();
-    PC_STAMP(5, 1);
-    // y pass: task (L, r) -> TY outputs of both Gaussians from one window row, read
-    // as NCP 16-byte vectors (padded or swizzled slots: conflict-free across lanes)
-    for (int t = tid; t < ly.nl * HX; t += NT) {
-        T v[NCP * VEC];
-#pragma unroll
-        for (int j = 0; j < NCP; ++j) {
-            const V x = reinterpret_cast<const V*>(s_in)[co_slot<NCP, LAYOUT>(t, j)];
-            if constexpr (VEC == 4) {
-                v[4 * j] = x.x; v[4 * j + 1] = x.y; v[4 * j + 2] = x.z; v[4 * j + 3] = x.w;
-            } else {
-                v[2 * j] = x.x; v[2 * j + 1] = x.y;
-            }
-        }
-#pragma unroll
-        for (int c = 0; c < TY; ++c) {
-            T e = 0, g = 0;
-#pragma unroll
-            for (int q = 0; q < FL; ++q) {
-                e += k.ge[q] * v[D + c + q];
-                g += k.gi[q] * v[D + c + q];
-            }
-            s_ye[t * TY + c] = e;
-            s_yi[t * TY + c] = g;
-        }
-    }
-#endif
     co_lds_barrier();
     PC_STAMP(5, 2);
     // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows
@@ -1510,13 +1464,12 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     }
     co_lds_barrier();
     PC_STAMP(5, 3);
-#if PC_CO_TVEC
     // theta pass: task (row i, column vector cv, chunk j) -> CO_TCL output layers of
     // VEC cells from CO_TCL + 6 x-pass layers read as 16-byte vectors; each output
     // layer leaves as one 16-byte store
     double sum = 0.0;
     {
-        constexpr int CL = PC_CO_TCL, NCV = TY / VEC;
+        constexpr int CL = CO_TCL, NCV = TY / VEC;
         const int ncl = (ly.nout + CL - 1) / CL;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
@@ -1554,42 +1507,6 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             }
         }
     }
-#else
-    // theta pass: task (cell p, chunk j) -> CO_CH output layers of one cell from
-    // CO_CH + 6 x-pass layers (lanes <-> cells: a wave reads 64 consecutive LDS words)
-    double sum = 0.0;
-    const int nch = (ly.nout + CO_CH - 1) / CO_CH;
-    for (int t = tid; t < TX * TY * nch; t += NT) {
-        const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
-        const int gi = x0 + i, gy = y0 + p - i * TY;
-        T xe[CO_CH + 2 * HALF], xi[CO_CH + 2 * HALF];
-#pragma unroll
-        for (int a = 0; a < CO_CH + 2 * HALF; ++a) {
-            const int L = ly.tap(j, a, TH);
-            xe[a] = s_xe[L * TX * TY + p];
-            xi[a] = s_xi[L * TX * TY + p];
-        }
-        const bool mine = gi < X && gy < Y;
-#pragma unroll
-        for (int o = 0; o < CO_CH; ++o) {
-            const int lo = j * CO_CH + o, gk = ly.k0 + lo;
-            T e = 0, g = 0;
-#pragma unroll
-            for (int q = 0; q < FL; ++q) {
-                e += k.ge[q] * xe[o + q];
-                g += k.gi[q] * xi[o + q];
-            }
-            const T v = (e - g) * k.scale;
-            const T qv = (v < k.inhib) ? T(0) : v - k.inhib;
-            if (mine && lo < ly.nout) {
-#ifndef PC_DIAG_NOSTORE  // diagnostic build of tools/pc_probe.hip only: no output stores
-                Q[((size_t)gk * X + gi) * Y + gy] = qv;
-#endif
-                sum += (double)qv;
-            }
-        }
-    }
-#endif
     sum = co_wave_sum(sum);
     if ((tid & 63) == 0) s_red[tid >> 6] = sum;
     co_lds_barrier();  // the Q stores drain meanwhile
@@ -1641,19 +1558,12 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         // window row (L, r) starts this many cells into its first vector
         s_yd[L] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
     }
-#if PC_CO_FTLATE
     // the filter table's loads are issued now and land in LDS behind the window's
     // (the first barrier waits for the shifts alone)
     constexpr int NFR = (RT_NFMAX * FT + NT - 1) / NT;
     T fr[NFR];
 #pragma unroll
     for (int u = 0; u < NFR; ++u) fr[u] = tid + u * NT < nf * FT ? filt[tid + u * NT] : T(0);
-#else
-    for (int i = tid; i < nf * FT; i += NT) {
-        const int fi = i / FT;
-        s_ftab[fi * ST_FTP + (i - fi * FT)] = filt[i];
-    }
-#endif
     T zf[FL];
 #pragma unroll
     for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
@@ -1663,13 +1573,8 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // c + d[L] of row (L, r), d[L] = (y0 - 3 + oy[L]) % Y % VEC
     using P0 = CoPart<HX, NCP>;
     constexpr int LPT = (THM * P0::PER_LAYER + NT - 1) / NT;
-    // PC_CO_PSPLIT: the window lands in two parts (loads u < UA, then the rest; vmcnt
-    // waits retire in issue order), and the layers complete in the first part are
-    // filtered while the second part's loads are still in flight
-    constexpr int UA = PC_CO_PSPLIT ? (LPT + 1) / 2 : LPT, UB = LPT - UA > 0 ? LPT - UA : 1;
-    typename CoVec<T>::type win[UA], win2[UB];
+    typename CoVec<T>::type win[LPT];
     co_issue<T, NT, HX, NCP, true, CHUNK, P0>(win, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
-    if constexpr (UA < LPT) co_issue<T, NT, HX, NCP, true, CHUNK, P0, UA>(win2, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < NPL; ++u) tot += pt[u];
@@ -1677,13 +1582,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     tot = co_wave_sum(tot);
     const T tt = (T)tot;
     co_store<NT, HX, NCP, CO_PLAIN, P0>(win, s_in, ly);
-#if PC_CO_FTLATE
 #pragma unroll
     for (int u = 0; u < NFR; ++u) {
         const int i = tid + u * NT, fi = i / FT;
         if (i < nf * FT) s_ftab[fi * ST_FTP + (i - fi * FT)] = fr[u];
     }
-#endif
     co_lds_barrier();
     PC_STAMP(6, 2);
     // 7x7 filter: task (L, column group, row part) -> TX/FS rows x CP columns of
@@ -1692,9 +1595,8 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // of them spills at 3 waves per SIMD)
     constexpr int FS = PC_CO_FSPLIT, TXH = TX / FS, CP = PC_CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    const int LA = UA < LPT ? min(ly.nl, (UA * NT) / P0::PER_LAYER) : ly.nl;
-    auto filter = [&](int t0, int t1) __attribute__((always_inline)) {
-        for (int t = tid + t0; t < t1; t += NT) {
+    {
+        for (int t = tid; t < ly.nl * NCG * FS; t += NT) {
             const int L = t / (FS * NCG), rem = t - L * FS * NCG, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
             T f[FT];
             st_filter<T>(s_ftab + s_fo[L], f);
@@ -1726,12 +1628,6 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                 for (int c = 0; c < CP; ++c)
                     s_p[(L * TX + hf * TXH + i) * TY + c0 + c] = acc[i][c] > T(0) ? acc[i][c] : T(0);
         }
-    };
-    filter(0, LA * NCG * FS);
-    if constexpr (UA < LPT) {
-        co_store<NT, HX, NCP, CO_PLAIN, P0, UA>(win2, s_in, ly);
-        co_lds_barrier();
-        filter(LA * NCG * FS, ly.nl * NCG * FS);
     }
     co_lds_barrier();
     PC_STAMP(6, 3);
@@ -1741,12 +1637,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     T bv = T(-1);
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
-#if PC_CO_TVEC
     {
         // task (row i, column vector cv, chunk j): CO_TCL output layers of VEC cells
         // from 16-byte LDS vectors, one 16-byte store per output layer
         using V = typename CoVec<T>::type;
-        constexpr int CL = PC_CO_TCL, NCV = TY / VEC;
+        constexpr int CL = CO_TCL, NCV = TY / VEC;
         const int ncl = (ly.nout + CL - 1) / CL;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
@@ -1788,38 +1683,6 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
             }
         }
     }
-#else
-    const int nch = (ly.nout + CO_CH - 1) / CO_CH;
-    for (int t = tid; t < TX * TY * nch; t += NT) {
-        const int j = t / (TX * TY), p = t - j * (TX * TY), i = p / TY;
-        const int gi = x0 + i, gy = y0 + p - i * TY;
-        T r[CO_CH + 2 * HALF];
-#pragma unroll
-        for (int a = 0; a < CO_CH + 2 * HALF; ++a) r[a] = s_p[ly.tap(j, a, TH) * TX * TY + p];
-        const bool mine = gi < X && gy < Y;
-#pragma unroll
-        for (int o = 0; o < CO_CH; ++o) {
-            const int lo = j * CO_CH + o, gk = ly.k0 + lo;
-            T v = 0;
-#pragma unroll
-            for (int z = 0; z < FL; ++z) v += r[o + z] * zf[z];
-            v = v > T(0) ? v : T(0);
-            if (tot != 0.0) v = v / tt;
-            if (mine && lo < ly.nout) {
-#ifndef PC_DIAG_NOSTORE
-                P[((size_t)gk * X + gi) * Y + gy] = v;
-#endif
-                const unsigned lin = ((unsigned)gi * Y + gy) * TH + gk;
-                if constexpr (sizeof(T) == 4) {
-                    bk = max(bk, argmax_key((float)v, lin));
-                } else if (v > bv || (v == bv && lin < bl)) {
-                    bv = v;
-                    bl = lin;
-                }
-            }
-        }
-    }
-#endif
     if constexpr (sizeof(T) == 4) {
         __shared__ unsigned long long s_bk[NW];
         bk = co_wave_max(bk);
@@ -1860,14 +1723,17 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 // Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
 // pinned host buffer (system-scope stores): one queued launch in place of a
 // device-to-host blit copy, which trailed the step by ~10 us (gap + copy kernel).
+// One wave per step: each lane takes the max of RES_SLOTS / 64 slots, then DPP.
 __global__ __launch_bounds__(64) void pc_res_export(const unsigned long long* __restrict__ res, int n,
                                                     unsigned long long* host) {
-    for (int s = blockIdx.x * 64 + threadIdx.x; s < n; s += gridDim.x * 64) {
+    static_assert(RES_SLOTS % 64 == 0, "slots per lane");
+    for (int s = blockIdx.x; s < n; s += gridDim.x) {
         const unsigned long long* r = res + (size_t)s * RES_SLOTS;
-        unsigned long long m = r[0];
+        unsigned long long m = r[threadIdx.x];
 #pragma unroll
-        for (int k = 1; k < RES_SLOTS; ++k) m = r[k] > m ? r[k] : m;
-        __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int k = 1; k < RES_SLOTS / 64; ++k) m = max(m, r[threadIdx.x + 64 * k]);
+        m = co_wave_max(m);
+        if (threadIdx.x == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2106,7 +1972,7 @@ int pc_grow_steps(rs_pc* h, int n) {
     RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
     RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
-    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * RES_SLOTS * cap,
+    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap,
                          hipHostMallocDefault));
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hResDev), h->hRes, 0));
     if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
@@ -2320,11 +2186,16 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
     RS_TRY(pc_grow_steps(h, n));
-    static const bool force_inline = [] {  // A/B: per-step control as kernel arguments in batches too
+    // Batches: the column form takes each step's control as kernel arguments too (its
+    // path kernel then starts its window loads without a global round trip for the
+    // shifts: 128x128x72 27.5 -> 27.1 us per step with the filter table staged behind
+    // the window); the other forms read the device ring (RS_PC_CTL=ring|inline overrides)
+    static const int ctl_env = [] {
         const char* e = std::getenv("RS_PC_CTL");
-        return e && std::strcmp(e, "inline") == 0;
+        return !e ? -1 : std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "ring") == 0 ? 0 : -1;
     }();
-    const bool inline_ctl = (n == 1 || force_inline) && h->TH <= CTL_INLINE_MAX;
+    const bool batch_inline = ctl_env >= 0 ? ctl_env == 1 : h->cols;
+    const bool inline_ctl = (n == 1 || batch_inline) && h->TH <= CTL_INLINE_MAX;
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
@@ -2354,7 +2225,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                            static_cast<const double*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
         RS_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(pc_res_export, dim3((n + 63) / 64 < 64 ? (n + 63) / 64 : 64), dim3(64), 0,
+    hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0,
                        h->stream, h->dRes, n, h->hResDev);
     RS_HIP(hipGetLastError());
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
