@@ -601,7 +601,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 #pragma unroll
     for (int u = 0; u < NPP; ++u) {
         const int i = tid + u * RT_NT;
-        pt[u] = i < npart ? part[i] : 0.0;
+        pt[u] = part[min(i, npart - 1)];  // unconditional (a guarded load got its wait hoisted)
     }
     double pextra = 0.0;  // npart beyond NPP * RT_NT (huge grids)
     for (int i = tid + NPP * RT_NT; i < npart; i += RT_NT) pextra += part[i];
@@ -657,7 +657,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     // publishes s_r
     double tot = pextra;
 #pragma unroll
-    for (int u = 0; u < NPP; ++u) tot += pt[u];
+    for (int u = 0; u < NPP; ++u) tot += tid + u * RT_NT < npart ? pt[u] : 0.0;
     tot = co_wave_sum(tot);
     if (lane == 0) s_red[wave] = tot;
     co_lds_barrier();
@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #pragma unroll
     for (int u = 0; u < NPP; ++u) {
         const int i = tid + u * NT;
-        pt[u] = i < npart ? part[i] : 0.0;
+        pt[u] = part[min(i, npart - 1)];  // unconditional (a guarded load got its wait hoisted)
     }
     double pextra = 0.0;
     for (int i = tid + NPP * NT; i < npart; i += NT) pextra += part[i];
@@ -1046,7 +1046,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     for (int d = 0; d < ST_PF; ++d) load(d, pre[d]);
     double tot = pextra;
 #pragma unroll
-    for (int u = 0; u < NPP; ++u) tot += pt[u];
+    for (int u = 0; u < NPP; ++u) tot += tid + u * NT < npart ? pt[u] : 0.0;
     tot = block_sum_w<NW>(tot, s_red);
     const T tt = (T)tot;
 
@@ -1545,18 +1545,23 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // the reduction after the window loads are issued waits for these alone).
     // Every wave forms the total itself: no block barrier between the window
     // loads' issue and their use.
+    // The control first (its loads are the ones the first barrier waits for; clamped
+    // unconditional reads, in flight together), then the partials (a guarded load
+    // had its wait hoisted to the kernel's start).
+    static_assert(THM <= NT, "one layer's control per thread");
+    const int Lc = min(tid, ly.nl - 1), gLc = ly.global(Lc, TH);
+    const int oxc = ctl_ox(ctl, gLc), oyc = ctl_oy(ctl, gLc), fic = ctl_fi(ctl, gLc);
     constexpr int NPL = 4;  // partials per lane loaded up front (npart <= 256 in one round)
     double pt[NPL];
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) pt[u] = lane + 64 * u < npart ? part[lane + 64 * u] : 0.0;
-    for (int L = tid; L < ly.nl; L += NT) {
-        const int gL = ly.global(L, TH);
-        s_ox[L] = rs::wrapi(ctl_ox(ctl, gL), X);  // shifts may exceed the grid (vtrans large)
-        const int oy = rs::wrapi(ctl_oy(ctl, gL), Y);
-        s_oy[L] = oy;
-        s_fo[L] = ctl_fi(ctl, gL) * ST_FTP;
+    for (int u = 0; u < NPL; ++u) pt[u] = part[min(lane + 64 * u, npart - 1)];
+    if (tid < ly.nl) {
+        s_ox[tid] = rs::wrapi(oxc, X);  // shifts may exceed the grid (vtrans large)
+        const int oy = rs::wrapi(oyc, Y);
+        s_oy[tid] = oy;
+        s_fo[tid] = fic * ST_FTP;
         // window row (L, r) starts this many cells into its first vector
-        s_yd[L] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
+        s_yd[tid] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
     }
     // the filter table's loads are issued now and land in LDS behind the window's
     // (the first barrier waits for the shifts alone)
@@ -1577,7 +1582,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     co_issue<T, NT, HX, NCP, true, CHUNK, P0>(win, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
     double tot = 0.0;
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) tot += pt[u];
+    for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
     for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
     tot = co_wave_sum(tot);
     const T tt = (T)tot;
