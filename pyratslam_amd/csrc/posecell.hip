@@ -1377,15 +1377,11 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
                                                           int X, int Y, int TH, int gx, int gy, int KC,
                                                           SepKernel<T> k) {
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
-    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, false>();
-    [[maybe_unused]] constexpr int LAYOUT = CHUNK ? CO_SWIZZLED : CO_PADDED;
-    constexpr int RP = (NCP + (CHUNK ? 0 : 1)) * VEC, WN = HX * RP;
-    constexpr int D = (VEC - HALF % VEC) % VEC;  // window column 0 within its row's first vector
-    static_assert(2 * TX * TY <= WN, "x-pass outputs alias the window");
-    static_assert(TY % VEC == 0 && D + HY <= NCP * VEC, "window row layout");
+    constexpr int VEC = co_vec<T>();
+    static_assert(TY % VEC == 0, "row vectors");
     __shared__ __attribute__((aligned(16))) T s_in[2 * THM * TX * TY];  // the x-pass outputs (e, i)
-    __shared__ T s_ye[THM * HX * TY];
-    __shared__ T s_yi[THM * HX * TY];
+    __shared__ __attribute__((aligned(16))) T s_ye[THM * HX * TY];  // [r][L][c]
+    __shared__ __attribute__((aligned(16))) T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
     using V = typename CoVec<T>::type;
     const int tid = threadIdx.x;
@@ -1395,44 +1391,45 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     if (res_slot != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += blockDim.x) res_slot[i] = 0ull;  // this step's path kernel max-reduces into them
     PC_STAMP(5, 0);
-    // y pass straight from the loads: task (L, r) = one window row per thread, its
-    // NCP 16-byte vectors loaded into registers (every row of the block in flight
-    // at once), TY outputs of both Gaussians into LDS; the window never visits LDS
+    // y pass straight from the loads.  P is theta-fastest on this form (cell (x, y)
+    // holds its TH layers contiguously), so task (r, L) = window row r of layer L
+    // puts consecutive lanes on consecutive layers: each load instruction reads
+    // consecutive words of one cell's theta column (whole 128-byte lines, where the
+    // layer-major rows of 14 cells used a third of each line they touched).  Every
+    // row of the block is in flight at once; the window never visits LDS; the y-pass
+    // outputs go to LDS as [r][L][c].
     {
         constexpr int NR = (THM * HX + NT - 1) / NT;
         const int nrow = ly.nl * HX;
-        V w[NR][NCP];
+        T w[NR][HY];
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
-            const int t = min(tid + u * NT, nrow - 1), L = t / HX, r = t - L * HX;
-            const T* row = P + (size_t)ly.global(L, TH) * X * Y + (size_t)co_wrap(x0 - HALF + r, X) * Y;
-            const int c0 = co_wrap(y0 - HALF, Y) & ~(VEC - 1);
+            const int t = min(tid + u * NT, nrow - 1), r = t / ly.nl, L = t - r * ly.nl;
+            const T* cell = P + ((size_t)co_wrap(x0 - HALF + r, X) * Y) * TH + ly.global(L, TH);
 #pragma unroll
-            for (int j = 0; j < NCP; ++j) w[u][j] = *reinterpret_cast<const V*>(row + co_wrap(c0 + j * VEC, Y));
+            for (int c = 0; c < HY; ++c) w[u][c] = cell[(size_t)co_wrap(y0 - HALF + c, Y) * TH];
         }
 #pragma unroll
         for (int u = 0; u < NR; ++u) {
             const int t = tid + u * NT;
             if (t >= nrow) break;
-            T v[NCP * VEC];
-#pragma unroll
-            for (int j = 0; j < NCP; ++j) {
-                if constexpr (VEC == 4) {
-                    v[4 * j] = w[u][j].x; v[4 * j + 1] = w[u][j].y; v[4 * j + 2] = w[u][j].z; v[4 * j + 3] = w[u][j].w;
-                } else {
-                    v[2 * j] = w[u][j].x; v[2 * j + 1] = w[u][j].y;
-                }
-            }
+            const int r = t / ly.nl, L = t - r * ly.nl;
+            V oe[TY / VEC], oi[TY / VEC];
 #pragma unroll
             for (int c = 0; c < TY; ++c) {
                 T e = 0, g = 0;
 #pragma unroll
                 for (int q = 0; q < FL; ++q) {
-                    e += k.ge[q] * v[D + c + q];
-                    g += k.gi[q] * v[D + c + q];
+                    e += k.ge[q] * w[u][c + q];
+                    g += k.gi[q] * w[u][c + q];
                 }
-                s_ye[t * TY + c] = e;
-                s_yi[t * TY + c] = g;
+                oe[c / VEC][c % VEC] = e;
+                oi[c / VEC][c % VEC] = g;
+            }
+#pragma unroll
+            for (int c = 0; c < TY / VEC; ++c) {
+                reinterpret_cast<V*>(s_ye + (r * THM + L) * TY)[c] = oe[c];
+                reinterpret_cast<V*>(s_yi + (r * THM + L) * TY)[c] = oi[c];
             }
         }
     }
@@ -1447,8 +1444,8 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
         T ye[HX], yi[HX];
 #pragma unroll
         for (int a = 0; a < HX; ++a) {
-            ye[a] = s_ye[(L * HX + a) * TY + c];
-            yi[a] = s_yi[(L * HX + a) * TY + c];
+            ye[a] = s_ye[(a * THM + L) * TY + c];
+            yi[a] = s_yi[(a * THM + L) * TY + c];
         }
 #pragma unroll
         for (int i = 0; i < TX; ++i) {
@@ -1531,7 +1528,12 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF;
     constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, true>(), RP = NCP * VEC, WN = HX * RP;
     __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] shifted windows
-    __shared__ T s_p[THM * TX * TY];   // clamped 7x7 outputs [L][i][c]
+    // clamped 7x7 outputs [cell p][SPO + L], pitch PP (16-byte rows: the theta pass
+    // reads VEC-aligned vectors); the whole-extent form also keeps wrapped copies of
+    // the last 4 layers before SPO and of the first 8 after SPO + TH, so every theta
+    // window is one contiguous aligned run
+    constexpr int SPO = 4, PP = (THM + 12 + 3) / 4 * 4;
+    __shared__ __attribute__((aligned(16))) T s_p[TX * TY * PP];
     __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_ox[THM], s_oy[THM], s_fo[THM], s_yd[THM];
     __shared__ T s_bv[NW];
@@ -1630,11 +1632,21 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
             for (int i = 0; i < TXH; ++i)
 #pragma unroll
-                for (int c = 0; c < CP; ++c)
-                    s_p[(L * TX + hf * TXH + i) * TY + c0 + c] = acc[i][c] > T(0) ? acc[i][c] : T(0);
+                for (int c = 0; c < CP; ++c) {
+                    s_p[((hf * TXH + i) * TY + c0 + c) * PP + SPO + L] = acc[i][c] > T(0) ? acc[i][c] : T(0);
+                }
         }
     }
     co_lds_barrier();
+    if constexpr (!CHUNK) {  // the wrapped copies: layers TH-4..TH-1 before, 0..7 after
+        for (int q = tid; q < TX * TY * 12; q += NT) {
+            const int p = q / 12, m = q - p * 12;
+            T* sp = s_p + p * PP + SPO;
+            if (m < 4) sp[m - 4] = sp[ly.nl - 4 + m];
+            else sp[ly.nl + m - 4] = sp[co_wrap(m - 4, ly.nl)];
+        }
+        co_lds_barrier();
+    }
     PC_STAMP(6, 3);
     // theta pass, clamp, normalisation, argmax: task (cell p, chunk j).  float32:
     // the first maximum as the largest packed (value, ~index) key; float64: value
@@ -1643,46 +1655,61 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
     {
-        // task (row i, column vector cv, chunk j): CO_TCL output layers of VEC cells
-        // from 16-byte LDS vectors, one 16-byte store per output layer
+        // task (cell p, group j of VEC layers), consecutive lanes on consecutive groups
+        // of one cell: P is theta-fastest on this form, so a group is one 16-byte
+        // store and a wave's stores cover consecutive cells' theta columns
         using V = typename CoVec<T>::type;
-        constexpr int CL = CO_TCL, NCV = TY / VEC;
-        const int ncl = (ly.nout + CL - 1) / CL;
+        const int ng = (ly.nout + VEC - 1) / VEC;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
-        for (int t = tid; t < TX * NCV * ncl; t += NT) {
-            const int j = t / (TX * NCV), rem = t - j * (TX * NCV), i = rem / NCV, cv = rem - i * NCV;
-            const int gi = x0 + i, gy = y0 + cv * VEC;
-            V r[CL + 2 * HALF];
+#pragma unroll 1
+        for (int t = tid; t < TX * TY * ng; t += NT) {
+            const int p = t / ng, j = t - p * ng, i = p / TY;
+            const int gi = x0 + i, gy = y0 + p - i * TY;
+            // taps of output lo = j * VEC + o: local layers lo - 3 .. lo + 3 (whole
+            // extent, from the aligned run starting at lo - 4) or lo .. lo + 6 (a chunk's
+            // local layer lo + 3 is its output lo)
+            constexpr int ROFF = CHUNK ? 0 : 1, NRV = (ROFF + VEC + 2 * HALF + VEC - 1) / VEC;
+            const V* sv = reinterpret_cast<const V*>(s_p + p * PP + SPO + j * VEC - (CHUNK ? 0 : 4));
+            T rr[NRV * VEC];
 #pragma unroll
-            for (int a = 0; a < CL + 2 * HALF; ++a)
-                r[a] = *reinterpret_cast<const V*>(s_p + (ly.tapc(j, a, CL, TH) * TX + i) * TY + cv * VEC);
-            const bool mine = gi < X && gy < Y;
+            for (int q = 0; q < NRV; ++q) {
+                const V x = sv[q];
 #pragma unroll
-            for (int o = 0; o < CL; ++o) {
-                const int lo = j * CL + o, gk = ly.k0 + lo;
-                V v = 0;
+                for (int c = 0; c < VEC; ++c) rr[q * VEC + c] = x[c];
+            }
+            const T* r = rr + ROFF;
+            V v;
 #pragma unroll
-                for (int z = 0; z < FL; ++z) v += r[o + z] * zf[z];
+            for (int o = 0; o < VEC; ++o) {
+                T x = 0;
 #pragma unroll
-                for (int c = 0; c < VEC; ++c) {
-                    T x = v[c] > T(0) ? v[c] : T(0);
-                    if (tot != 0.0) x = x / tt;
-                    v[c] = x;
-                }
-                if (mine && lo < ly.nout) {
+                for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
+                x = x > T(0) ? x : T(0);
+                if (tot != 0.0) x = x / tt;
+                v[o] = x;
+            }
+            if (gi < X && gy < Y) {
+                const int gk0 = ly.k0 + j * VEC, nv = min(VEC, ly.nout - j * VEC);
+                const size_t e0 = ((size_t)gi * Y + gy) * TH + gk0;
 #ifndef PC_DIAG_NOSTORE
-                    co_put(P, ((size_t)gk * X + gi) * Y + gy, v, wt, nbytes);
+                if (nv == VEC && e0 % VEC == 0) {
+                    co_put(P, e0, v, wt, nbytes);
+                } else {  // a ragged or unaligned group (TH or the chunk not a multiple of VEC)
+#pragma unroll
+                    for (int o = 0; o < VEC; ++o)
+                        if (o < nv) P[e0 + o] = v[o];
+                }
 #endif
 #pragma unroll
-                    for (int c = 0; c < VEC; ++c) {
-                        const unsigned lin = ((unsigned)gi * Y + gy + c) * TH + gk;
-                        if constexpr (sizeof(T) == 4) {
-                            bk = max(bk, argmax_key((float)v[c], lin));
-                        } else if (v[c] > bv || (v[c] == bv && lin < bl)) {
-                            bv = v[c];
-                            bl = lin;
-                        }
+                for (int o = 0; o < VEC; ++o) {
+                    if (o >= nv) break;
+                    const unsigned lin = (unsigned)(e0 + o);
+                    if constexpr (sizeof(T) == 4) {
+                        bk = max(bk, argmax_key((float)v[o], lin));
+                    } else if (v[o] > bv || (v[o] == bv && lin < bl)) {
+                        bv = v[o];
+                        bl = lin;
                     }
                 }
             }
@@ -1814,7 +1841,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_steps(const T* __restrict__ bmax
 template <typename T>
 __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, int X, int Y, int TH,
                                                        T* __restrict__ bmax,
-                                                       unsigned* __restrict__ bidx) {
+                                                       unsigned* __restrict__ bidx, int thfast) {
     __shared__ T s_bv[NT];
     __shared__ unsigned s_bl[NT];
     const size_t n = (size_t)X * Y * TH;
@@ -1825,7 +1852,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, 
         const int rem = (int)(e - (size_t)k * X * Y);
         const int i = rem / Y, j = rem - i * Y;
         const T v = P[e];
-        const unsigned lin = ((unsigned)i * Y + j) * TH + k;
+        const unsigned lin = thfast ? (unsigned)e : ((unsigned)i * Y + j) * TH + k;
         if (v > bv || (v == bv && lin < bl)) {
             bv = v;
             bl = lin;
@@ -1851,31 +1878,40 @@ __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, 
     }
 }
 
+// Element e of the C-order (x, y, th) volume -> its place in a layer-major volume
+// (or itself in a theta-fastest one: the column form's P, which is C order).
+__device__ inline size_t pc_layer_major(size_t e, int X, int Y, int TH) {
+    const int k = (int)(e % TH);
+    const size_t xy = e / TH;
+    const int j = (int)(xy % Y), i = (int)(xy / Y);
+    return ((size_t)k * X + i) * Y + j;
+}
+
 template <typename T>
 __global__ void pc_export_kernel(const T* __restrict__ P, double* __restrict__ out, int X, int Y,
-                                 int TH) {
+                                 int TH, int thfast) {
     const size_t n = (size_t)X * Y * TH;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
-         e += (size_t)gridDim.x * blockDim.x) {
-        // e indexes the C-order (x, y, th) output
-        const int k = (int)(e % TH);
-        const size_t xy = e / TH;
-        const int j = (int)(xy % Y), i = (int)(xy / Y);
-        out[e] = (double)P[((size_t)k * X + i) * Y + j];
-    }
+         e += (size_t)gridDim.x * blockDim.x)
+        out[e] = (double)P[thfast ? e : pc_layer_major(e, X, Y, TH)];
 }
 
 template <typename T>
 __global__ void pc_import_kernel(const double* __restrict__ in, T* __restrict__ P, int X, int Y,
-                                 int TH) {
+                                 int TH, int thfast) {
     const size_t n = (size_t)X * Y * TH;
     for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
-         e += (size_t)gridDim.x * blockDim.x) {
-        const int k = (int)(e % TH);
-        const size_t xy = e / TH;
-        const int j = (int)(xy % Y), i = (int)(xy / Y);
-        P[((size_t)k * X + i) * Y + j] = (T)in[e];
-    }
+         e += (size_t)gridDim.x * blockDim.x)
+        P[thfast ? e : pc_layer_major(e, X, Y, TH)] = (T)in[e];
+}
+
+// layer-major Q -> theta-fastest P (the column form's rs_pc_excite: P = normalised Q)
+template <typename T>
+__global__ void pc_relayout_kernel(const T* __restrict__ Q, T* __restrict__ P, int X, int Y, int TH) {
+    const size_t n = (size_t)X * Y * TH;
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
+         e += (size_t)gridDim.x * blockDim.x)
+        P[e] = Q[pc_layer_major(e, X, Y, TH)];
 }
 
 template <typename T>
@@ -1948,7 +1984,8 @@ struct rs_pc {
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
-    bool cols = false;      // column kernels (RS_PC_FORM=cols[:KC]): TX x TY tiles through KC layers
+    bool cols = false;      // column kernels (RS_PC_FORM=cols[:KC]): TX x TY tiles through KC layers;
+                            // P is then theta-fastest (C order (x, y, th)), Q layer-major
     int cgx = 0, cgy = 0;   // column tiles along x and y
     int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
@@ -2293,7 +2330,7 @@ int pc_argmax_impl(rs_pc* h, int32_t* out) {
     const int nb = h->nBmaxCap < 1024 ? h->nBmaxCap : 1024;
     hipLaunchKernelGGL((pc_argmax_blocks<T>), dim3(nb), dim3(NT), 0, h->stream,
                        static_cast<const T*>(h->dP), h->X, h->Y, h->TH, static_cast<T*>(h->dBmax),
-                       h->dBidx);
+                       h->dBidx, (int)h->cols);
     RS_HIP(hipGetLastError());
     hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
                        static_cast<const T*>(h->dBmax), h->dBidx, nb, h->dRes);
@@ -2629,7 +2666,18 @@ int rs_pc_excite(rs_pc* h) {
                            static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
     }
     RS_HIP(hipGetLastError());
-    RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
+    if (h->cols) {  // P is theta-fastest on the column form, Q layer-major
+        if (h->prec == RS_PREC_F32)
+            hipLaunchKernelGGL((pc_relayout_kernel<float>), dim3(256), dim3(NT), 0, h->stream,
+                               static_cast<const float*>(h->dQ), static_cast<float*>(h->dP), h->X, h->Y, h->TH);
+        else
+            hipLaunchKernelGGL((pc_relayout_kernel<double>), dim3(256), dim3(NT), 0, h->stream,
+                               static_cast<const double*>(h->dQ), static_cast<double*>(h->dP), h->X, h->Y,
+                               h->TH);
+        RS_HIP(hipGetLastError());
+    } else {
+        RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
+    }
     RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
 }
@@ -2751,7 +2799,8 @@ int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th) {
     RS_CHECK(x >= 0 && x < h->X && y >= 0 && y < h->Y && th >= 0 && th < h->TH, RS_ERR_ARG,
              "inject location (%d, %d, %d) outside grid (%d, %d, %d)", x, y, th, h->X, h->Y, h->TH);
     RS_HIP(hipSetDevice(h->device));
-    const size_t idx = ((size_t)th * h->X + x) * h->Y + y;
+    // the column form keeps P theta-fastest (C order); the others layer-major
+    const size_t idx = h->cols ? ((size_t)x * h->Y + y) * h->TH + th : ((size_t)th * h->X + x) * h->Y + y;
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_inject_kernel<float>), dim3(1), dim3(64), 0, h->stream,
                            static_cast<float*>(h->dP), idx, energy);
@@ -2778,10 +2827,10 @@ int rs_pc_read(rs_pc* h, double* host) {
     RS_HIP(hipSetDevice(h->device));
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_export_kernel<float>), dim3(256), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH);
+                           static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)h->cols);
     else
         hipLaunchKernelGGL((pc_export_kernel<double>), dim3(256), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH);
+                           static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)h->cols);
     RS_HIP(hipGetLastError());
     RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
@@ -2795,10 +2844,10 @@ int rs_pc_write(rs_pc* h, const double* host) {
     RS_HIP(hipMemcpyAsync(h->dTmp, host, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_import_kernel<float>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
-                           static_cast<float*>(h->dP), h->X, h->Y, h->TH);
+                           static_cast<float*>(h->dP), h->X, h->Y, h->TH, (int)h->cols);
     else
         hipLaunchKernelGGL((pc_import_kernel<double>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
-                           static_cast<double*>(h->dP), h->X, h->Y, h->TH);
+                           static_cast<double*>(h->dP), h->X, h->Y, h->TH, (int)h->cols);
     RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
