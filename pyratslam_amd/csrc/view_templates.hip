@@ -560,26 +560,17 @@ __device__ __forceinline__ void plane_rows(const uint32_t (&P)[PlaneRange<H, HAL
     if constexpr (S < R::SB) plane_rows<H, HALF, S + 1>(P, sq, acc);
 }
 
-#ifndef PL_ONEBAR
-#define PL_ONEBAR 1
-#endif
 
 template <int H>
 struct PlaneLds {
     static constexpr int M = FAST_M, NS = H - 2 * M + 3, NO = 2 * M - 1, NK = (NO + 1) / 2;
     static constexpr int QW = PL_CG * NS * 8;                 // query-plane dwords per query
     static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
-#if PL_ONEBAR
     // double-buffered: batch i computes from q[i&1] and adds its partial counts into
     // part[i&1] while batch i+1 is staged into q[(i+1)&1]; one barrier per batch
     uint4 q[2][PL_NB * QW / 4];
     uint32_t part[2][PL_NB][NK][64];                           // u16 pairs, summed by ds_add
     int bidx[3];                                               // batches taken ahead (ring)
-#else
-    uint4 q[PL_NB * QW / 4];                                   // the batch's query planes
-    uint32_t part[PL_NB][NK][NW][64];                          // u16 pairs: offsets 2k, 2k+1
-    int batch;
-#endif
     uint32_t ts[16][64];                                       // TS(o) of the 64 templates
 };
 
@@ -596,7 +587,6 @@ __device__ __forceinline__ void plane_load_units(const uint4* __restrict__ plane
     }
 }
 
-#if PL_ONEBAR
 // The work of one wave: column group cg, query start rows of range HALF.  One
 // barrier per batch: before it, every wave stages its share of the next batch's
 // planes and adds this batch's partial counts into LDS (ds_add; the per-half
@@ -665,65 +655,6 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
         bi = bn;
     }
 }
-#else
-// The work of one wave: column group cg, query start rows of range HALF.
-template <int H, int HALF, bool MATRIX>
-__device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
-                                           int tb, int64_t count, const uint4* __restrict__ qp4,
-                                           const uint32_t* __restrict__ qsum, int nq,
-                                           unsigned* __restrict__ ctr, int G, int g, ScanOut out,
-                                           int rank, int nranks, int wave, int cg, int lane,
-                                           unsigned& failed) {
-    using R = PlaneRange<H, HALF>;
-    using LD = PlaneLds<H>;
-    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
-    uint32_t P[R::NUH][8];
-    plane_load_units<H, HALF>(planes, tb, cg, lane, P);
-    // this block's query group g of G: batches g, g + G, g + 2G, ...
-    const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
-    const int64_t slot = (int64_t)tb * 64 + lane;
-    const int tid = wave * 64 + lane;
-    for (;;) {
-        // two barriers per batch: (A) staged planes visible, (B) partial counts
-        // visible; the next batch is taken during the compute (L.batch is read
-        // before (A) and rewritten after it)
-        const int bi = L.batch;
-        if (bi >= nbatch) break;  // block-uniform
-        const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
-        for (int i = tid; i < nb * LD::QW / 4; i += NT) L.q[i] = qp4[(size_t)qb * (LD::QW / 4) + i];
-        __syncthreads();  // (A)
-        if (tid == 0) {
-            L.batch = (int)atomicAdd(ctr, 1u);
-            if (L.batch >= nbatch) failed = (unsigned)L.batch;
-        }
-#pragma unroll 1
-        for (int b = 0; b < nb; ++b) {
-            uint32_t acc[NO];
-#pragma unroll
-            for (int o = 0; o < NO; ++o) acc[o] = 0u;
-            plane_rows<H, HALF, R::SA>(
-                P, reinterpret_cast<const uint32_t*>(L.q) + (b * PL_CG + cg) * NS * 8, acc);
-#pragma unroll
-            for (int k = 0; k < NK; ++k)
-                L.part[b][k][wave][lane] = acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u);
-        }
-        __syncthreads();  // (B)
-        if (wave < nb) {  // wave w finishes query qb + w of the batch
-            const int qi = qb + wave;
-            uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < NK; ++k) {
-                uint32_t t = 0;  // per-half sums stay < 2^16: no carry between the halves
-#pragma unroll
-                for (int w = 0; w < LD::NW; ++w) t += L.part[wave][k][w][lane];
-                best = min(best, L.ts[2 * k][lane] + 256u * (t & 0xFFFFu));
-                if (2 * k + 1 < NO) best = min(best, L.ts[2 * k + 1][lane] + 256u * (t >> 16));
-            }
-            emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
-        }
-    }
-}
-#endif
 
 // nqc blocks serve each template block; they take query batches of PL_NB from
 // the template block's counter, so blocks that the SIMDs' oldest-first issue
@@ -750,7 +681,6 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
     unsigned failed = 0u;  // thread 0: the value of this block's one failed take
-#if PL_ONEBAR
     for (int i = threadIdx.x; i < 2 * PL_NB * PlaneLds<H>::NK * 64; i += blockDim.x)
         (&L.part[0][0][0][0])[i] = 0u;
     if (threadIdx.x == 0) {  // the first batch and the one after it
@@ -772,12 +702,6 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
         const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
         for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) L.q[0][i] = qp4[(size_t)qb * QW4 + i];
     }
-#else
-    if (threadIdx.x == 0) {
-        L.batch = (int)atomicAdd(ctr, 1u);
-        if (L.batch >= nbatch) failed = (unsigned)L.batch;
-    }
-#endif
     __syncthreads();
     const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
     if (half == 0)
