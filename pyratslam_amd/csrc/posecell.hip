@@ -1168,7 +1168,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 // Y >= TY+6 (checked on the host); TH <= co_thmax (the window in LDS).
 // ---------------------------------------------------------------------------
 #ifndef PC_CO_NW
-#define PC_CO_NW 9
+#define PC_CO_NW 12  // 9, 10, 11, 13, 14, 16: 20.6, 20.3, 20.2, 20.5, 20.3, 20.2 us vs 19.8 at 128x128x72
 #endif
 #ifndef PC_CO_TX
 #define PC_CO_TX 8
@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #ifndef PC_CO_FCOLS
 #define PC_CO_FCOLS 2   // 7x7 filter: output columns per task
 #endif
-// 9 waves: TH*TY = 576 x-pass tasks at TH = 72 (-D overrides for A/B builds of the probe)
+// 12 waves per block (768 threads; -D overrides for A/B builds of the probe)
 constexpr int CO_TX = PC_CO_TX, CO_TY = 8, CO_NW = PC_CO_NW;
 constexpr int CO_CH = 8;                        // layers per theta-pass task (scalar stream/rows helpers)
 constexpr int CO_TCL = 2;                       // column theta passes: output layers per task

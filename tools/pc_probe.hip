@@ -148,7 +148,7 @@ int main(int argc, char** argv) {
         hipEvent_t c0, c1;
         CK(hipEventCreate(&c0));
         CK(hipEventCreate(&c1));
-        const dim3 g(h->cgx * h->cgy), b(64 * CO_NW);
+        const dim3 g(h->cgx * h->cgy), b(64 * CO_NW), bp(64 * CO_NW);
         constexpr int THF = co_thmax<float>();
         const int reps = 500;
         float t = 0;
@@ -170,7 +170,7 @@ int main(int argc, char** argv) {
         printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, THF, false, PcCtlRing>), g, b, 0, h->stream,
+            hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, THF, false, PcCtlRing>), g, bp, 0, h->stream,
                                (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
                                (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
                                (unsigned*)nullptr, X, Y, TH, h->cgx, h->cgy, h->coKC);
