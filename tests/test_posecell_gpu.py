@@ -112,10 +112,13 @@ def test_large_grid_properties(pcn):
     assert np.abs(pa - pb).max() < F32_TOL
 
 
-def test_keyerror_leaves_reference_state(pcn):
+@pytest.mark.parametrize('form', ['', 'cols'])   # cols: P theta-fastest, Q layer-major
+def test_keyerror_leaves_reference_state(pcn, monkeypatch, form):
+    monkeypatch.setenv('RS_PC_FORM', form)
     case = load_golden('pc_keyerror')
     shape = tuple(case['shape'])
     net = pcn(shape, precision='float64')
+    assert not form or net.step_form() == form
     net.inject(1, (16, 16, 9))
     with pytest.raises(KeyError) as e:
         net.update(case['odom'][0])
@@ -136,11 +139,15 @@ def test_keyerror_leaves_reference_state(pcn):
     assert np.abs(net2.posecells - ref2.posecells).max() < F64_TOL
 
 
-def test_state_roundtrip_inject_and_argmax(pcn):
+# the default form at 21x21x36, and the column form (P theta-fastest) at a ragged
+# grid whose theta extent is not a multiple of the 16-byte groups
+@pytest.mark.parametrize('form,shape', [('', (21, 21, 36)), ('cols', (24, 40, 13)), ('cols', (32, 32, 20))])
+def test_state_roundtrip_inject_and_argmax(pcn, monkeypatch, form, shape):
+    monkeypatch.setenv('RS_PC_FORM', form)
     rng = np.random.default_rng(3)
-    shape = (21, 21, 36)
     for precision in ('float32', 'float64'):
         net = pcn(shape, precision=precision)
+        assert not form or net.step_form() == form
         assert (net.posecells == 0).all()
         assert net.get_pc_max() == (0, 0, 0)          # argmax of zeros = first cell
         v = rng.random(shape)
