@@ -1,4 +1,8 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
-timeout -k 10 500 python -u tools/pc_ab.py abtmp/final.so abtmp/fs4.so abtmp/fc4.so abtmp/fs1.so abtmp/fr1.so --rounds 3 > gpurun_out/pc_ab19.log 2>&1
-rc=$?; tail -5 gpurun_out/pc_ab19.log; exit $rc
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/gpu_tests.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke.log; if fatal $rc; then exit $rc; fi
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err
+rc=$?; tail -c 200 gpurun_out/bench.log; exit $rc
