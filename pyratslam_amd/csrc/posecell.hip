@@ -526,7 +526,8 @@ __global__ __launch_bounds__(RT_NT) void pc_excite_rows(const T* __restrict__ P,
                 }
                 const T val = (e - g) * k.scale;
                 const T q = (val < k.inhib) ? T(0) : val - k.inhib;
-                Q[((size_t)gk * X + gi) * Y + j] = q;
+                // write-through (sc1): nothing dirty left for the kernel's end to write back
+                __hip_atomic_store(&Q[((size_t)gk * X + gi) * Y + j], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 sum += (double)q;
             }
         }
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * (T)ctl_zf(ctl, z);
                 T val = acc > T(0) ? acc : T(0);
                 if (tot != 0.0) val = val / tt;
-                P[((size_t)gk * X + gi) * Y + j] = val;
+                __hip_atomic_store(&P[((size_t)gk * X + gi) * Y + j], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
                 if constexpr (sizeof(T) == 4) {
                     bk = max(bk, argmax_key((float)val, lin));
