@@ -568,7 +568,8 @@ struct PlaneLds {
     static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
     // double-buffered: batch i computes from q[i&1] and adds its partial counts into
     // part[i&1] while batch i+1 is staged into q[(i+1)&1]; one barrier per batch
-    uint4 q[2][PL_NB * QW / 4];
+    static constexpr int QP = (PL_NB * QW / 4 + 63) / 64 * 64;  // padded to whole 1 KiB wave-instructions
+    uint4 q[2][QP];
     uint32_t part[2][PL_NB][NK][64];                           // u16 pairs, summed by ds_add
     int bidx[3];                                               // batches taken ahead (ring)
     uint32_t ts[16][64];                                       // TS(o) of the 64 templates
@@ -606,6 +607,7 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
     constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
     uint32_t P[R::NUH][8];
     plane_load_units<H, HALF>(planes, tb, cg, lane, P);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the template planes have landed before the loop
     const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     const int64_t slot = (int64_t)tb * 64 + lane;
     const int tid = wave * 64 + lane;
@@ -617,16 +619,27 @@ __device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restri
         const int cur = it & 1, nxt = cur ^ 1, r1 = (it + 1) % 3, r2 = (it + 2) % 3;
         const int bn = L.bidx[r1];
         const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
-        if (bn < nbatch) {  // stage the next batch (its buffer's last readers passed the previous barrier)
+        // the next batch's planes go global -> LDS directly (global_load_lds, 1 KiB per
+        // wave-instruction, lane-linear), in flight through this batch's compute; the
+        // barrier's vmcnt(0) retires them.  The take comes first (its result is waited for);
+        // with no next batch there is no further take: this block's failed take was bn.
+        if (tid == 0) {  // the batch after next
+            const unsigned t = bn < nbatch ? atomicAdd(ctr, 1u) : (unsigned)nbatch;
+            L.bidx[r2] = (int)t;
+            if (bn < nbatch && (int)t >= nbatch) failed = t;
+        }
+        if (bn < nbatch) {
             const int qn = (bn * G + g) * PL_NB, nbn = min(PL_NB, nq - qn);
-            for (int i = tid; i < nbn * LD::QW / 4; i += NT) L.q[nxt][i] = qp4[(size_t)qn * (LD::QW / 4) + i];
-            if (tid == 0) {  // the batch after next
-                const unsigned t = atomicAdd(ctr, 1u);
-                L.bidx[r2] = (int)t;
-                if ((int)t >= nbatch) failed = t;
+            const int lim = nbn * LD::QW / 4;
+            const uint4* src = qp4 + (size_t)qn * (LD::QW / 4);
+#pragma unroll
+            for (int k = 0; k < (LD::QP + NT - 1) / NT; ++k) {
+                const int i0 = wave * 64 + k * NT;  // wave-uniform
+                if (i0 < lim)
+                    __builtin_amdgcn_global_load_lds(
+                        (__attribute__((address_space(1))) const void*)(src + min(i0 + lane, lim - 1)),
+                        (__attribute__((address_space(3))) void*)(&L.q[nxt][i0]), 16, 0, 0);
             }
-        } else if (tid == 0) {
-            L.bidx[r2] = nbatch;  // no further take: this block's failed take was bn
         }
 #pragma unroll 1
         for (int b = 0; b < nb; ++b) {

@@ -53,3 +53,23 @@ def test_checker_flags_a_reused_load_destination():
     hits = H.scan(name, body, asm_only=True)
     kinds = sorted(k for _, k, _, _, _ in hits)
     assert kinds == ['read', 'write'], hits
+
+
+def test_checker_lds_dma_has_no_register_destination():
+    """global_load_lds reads its address VGPRs at issue and writes none, so they may
+    be reused at once; it still counts in vmcnt for the loads issued before it."""
+    import asm_load_hazards as H
+    listing = '''_Zkernel:
+\tglobal_load_dword v7, v[2:3], off
+\tglobal_load_lds_dwordx4 v[80:81], off
+\tv_min_i32_e32 v80, s50, v98
+\ts_waitcnt vmcnt(1)
+\tv_add_u32_e32 v9, v7, v7
+\ts_endpgm
+.Lfunc_end0:
+'''.splitlines()
+    (name, body), = list(H.kernels(listing))
+    assert H.scan(name, body, asm_only=False) == []
+    # with vmcnt(2) the plain load may still be in flight: its destination read is flagged
+    body2 = [ln.replace('vmcnt(1)', 'vmcnt(2)') for ln in body]
+    assert [k for _, k, _, _, _ in H.scan(name, body2, asm_only=False)] == ['read']

@@ -75,7 +75,11 @@ def scan(name, body, asm_only):
             continue
         m = LOAD.match(s)
         ops = s.split(None, 1)[1] if ' ' in s else ''
-        if m:
+        if m and ('_lds' in s.split()[0] or re.search(r'\blds\b', ops)):
+            # LDS-DMA (global_load_lds_*, buffer_load ... lds): no VGPR destination, the
+            # operands are addresses read at issue; it still holds a vmcnt slot
+            dest, srcs = set(), regs(ops)
+        elif m:
             dest = regs(m.group(2))
             srcs = regs(ops[len(m.group(2)):])
         else:
