@@ -161,9 +161,22 @@ int rs_pc_last_ms(rs_pc* h, double* ms);
  * around every launch on the handle's stream; only when profiling is enabled) */
 int rs_pc_set_profiling(rs_pc* h, int enable);
 int rs_pc_kernel_ms(rs_pc* h, double ms[2]);
-/* step kernels in use: "rows" (row-tiled excite + path launches, Y <= 128) or
- * "tiles" (3-D tiles, any Y) */
+/* step kernels in use: "rows" (row-tiled excite + path launches, Y <= 128),
+ * "cols" (column tiles through all layers, large grids), "stream" (layer
+ * streaming, large grids outside the column form's limits) or "tiles" (3-D tiles) */
 const char* rs_pc_step_form(const rs_pc* h);
+/* Test hooks (no reference counterpart):
+ *   RS_PC_DBG_POISON       fill every buffer a step writes before it reads (the
+ *                          excited volume, the normalisation partials, the argmax
+ *                          slots and partials, the host result words) with all
+ *                          bits set, so that a read of anything the step did not
+ *                          write shows up as NaN state or a wrong peak;
+ *   RS_PC_DBG_SKIP_EXPORT  the next update/run leaves the host result words
+ *                          unwritten: the call must fail with RS_ERR_HIP (the
+ *                          check that every step's argmax reached the host). */
+#define RS_PC_DBG_POISON      1
+#define RS_PC_DBG_SKIP_EXPORT 2
+int rs_pc_debug(rs_pc* h, int op);
 
 /* ------------------------------------------------------------------------ */
 /* View templates                                                            */

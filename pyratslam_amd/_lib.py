@@ -24,6 +24,8 @@ RS_ERR_NOMEM = 7
 RS_ERR_CTL_RANGE = 8
 RS_PREC_F32 = 0
 RS_PREC_F64 = 1
+RS_PC_DBG_POISON = 1
+RS_PC_DBG_SKIP_EXPORT = 2
 RS_VT_FROZEN = 0
 RS_VT_SEQUENTIAL = 1
 RS_UNIQUE_ID_BYTES = 128
@@ -86,6 +88,7 @@ SIGNATURES = {
     'rs_pc_set_profiling': (ctypes.c_int, [_vp, ctypes.c_int]),
     'rs_pc_kernel_ms': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_step_form': (ctypes.c_char_p, [_vp]),
+    'rs_pc_debug': (ctypes.c_int, [_vp, ctypes.c_int]),
     'rs_vt_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
     'rs_vt_destroy': (ctypes.c_int, [_vp]),

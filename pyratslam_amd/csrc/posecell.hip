@@ -80,6 +80,11 @@ __device__ inline double ctl_zf(const PcCtlRing& c, int z) { return c.zf[z]; }
 // held each step's end back: 64x64x36 13.35 -> 12.32 us per batched step,
 // 128x128x72 27.7 -> 26.8, tools/pc_ab.py).
 constexpr int RES_SLOTS = 256;
+// No step's packed key is ever 0: float32 keys are (value bits << 32 | ~lin) and
+// float64 keys ~lin, with lin < X*Y*TH < 2^32 - 1 (rs_pc_create).  The host writes
+// RES_NONE into each step's result word before the launch and refuses a result
+// still holding it after the stream has synchronised.
+constexpr unsigned long long RES_NONE = 0ull;
 __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
     return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
 }
@@ -1996,6 +2001,7 @@ struct rs_pc {
     OdoTables odo{};
     std::vector<int32_t> cOx, cOy, cRows;
     std::vector<double> cZf;
+    bool dbgSkipExport = false;  // rs_pc_debug(RS_PC_DBG_SKIP_EXPORT): the next run leaves hRes unwritten
 };
 
 namespace {
@@ -2015,8 +2021,15 @@ int pc_grow_steps(rs_pc* h, int n) {
     RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
     RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
     RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
+    // every slot starts zeroed (the excitation's block 0 zeroes a step's slots again
+    // before its path kernel max-reduces into them; no step ever reads freed data)
+    RS_HIP(hipMemsetAsync(h->dRes, 0, sizeof(unsigned long long) * RES_SLOTS * cap, h->stream));
+    // the export kernel stores each step's key here with a system-scope store:
+    // fine-grained (coherent) host memory, so the store is visible once the stream
+    // has synchronised; pc_run_impl also checks a sentinel per step (RES_NONE)
     RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap,
-                         hipHostMallocDefault));
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    for (int s = 0; s < cap; ++s) h->hRes[s] = RES_NONE;
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hResDev), h->hRes, 0));
     if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
         RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
@@ -2268,11 +2281,19 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                            static_cast<const double*>(h->dArgV), h->dArgI, h->nPathBlocks, h->dRes);
         RS_HIP(hipGetLastError());
     }
-    hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0,
-                       h->stream, h->dRes, n, h->hResDev);
-    RS_HIP(hipGetLastError());
+    for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
+    if (!h->dbgSkipExport) {
+        hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0,
+                           h->stream, h->dRes, n, h->hResDev);
+        RS_HIP(hipGetLastError());
+    }
+    h->dbgSkipExport = false;
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    for (int s = 0; s < n; ++s)
+        RS_CHECK(h->hRes[s] != RES_NONE, RS_ERR_HIP,
+                 "step %d of %d: its argmax key did not reach the host result buffer after the "
+                 "stream synchronised", s, n);
     if (h->profiling) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     else h->lastMs = 0.f;  // the step-bracketing events are recorded only while profiling
     if (h->profiling) {
@@ -2587,7 +2608,12 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     PC_ALLOC(hipMalloc(&h->dP, h->n * h->esz));
     PC_ALLOC(hipMalloc(&h->dQ, h->n * h->esz));
     PC_ALLOC(hipMemsetAsync(h->dP, 0, h->n * h->esz, h->stream));  // zeros(shape), :27
+    // Q and the partials are rewritten in full by every excitation before a path
+    // kernel reads them; zeroed anyway so that no launch can see a freed handle's data
+    // (rs_pc_debug(RS_PC_DBG_POISON) + tests/test_posecell_gpu.py check the former)
+    PC_ALLOC(hipMemsetAsync(h->dQ, 0, h->n * h->esz, h->stream));
     PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart));
+    PC_ALLOC(hipMemsetAsync(h->dPart, 0, sizeof(double) * h->nPart, h->stream));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
@@ -2894,6 +2920,32 @@ const char* rs_pc_step_form(const rs_pc* h) {
     if (h->streamed) return "stream";
     if (h->cols) return "cols";
     return h->tiling ? "rows" : "tiles";
+}
+
+int rs_pc_debug(rs_pc* h, int op) {
+    rs::clear_error();
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_HIP(hipSetDevice(h->device));
+    if (op == RS_PC_DBG_POISON) {
+        // every buffer a step writes before it reads: all bits set (NaN volumes, the
+        // largest possible argmax key in every slot of every step)
+        RS_HIP(hipMemsetAsync(h->dQ, 0xFF, h->n * h->esz, h->stream));
+        RS_HIP(hipMemsetAsync(h->dPart, 0xFF, sizeof(double) * h->nPart, h->stream));
+        RS_HIP(hipMemsetAsync(h->dRes, 0xFF, sizeof(unsigned long long) * RES_SLOTS * h->resCap, h->stream));
+        RS_HIP(hipMemsetAsync(h->dBmax, 0xFF, h->esz * h->nBmaxCap, h->stream));
+        RS_HIP(hipMemsetAsync(h->dBidx, 0xFF, sizeof(unsigned) * h->nBmaxCap, h->stream));
+        if (h->dArgV) RS_HIP(hipMemsetAsync(h->dArgV, 0xFF, h->esz * (size_t)h->resCap * h->nPathBlocks, h->stream));
+        if (h->dArgI)
+            RS_HIP(hipMemsetAsync(h->dArgI, 0xFF, sizeof(unsigned) * (size_t)h->resCap * h->nPathBlocks, h->stream));
+        for (int s = 0; s < h->resCap; ++s) h->hRes[s] = ~0ull;
+        RS_HIP(hipStreamSynchronize(h->stream));
+        return RS_OK;
+    }
+    if (op == RS_PC_DBG_SKIP_EXPORT) {
+        h->dbgSkipExport = true;
+        return RS_OK;
+    }
+    RS_CHECK(false, RS_ERR_ARG, "unknown rs_pc_debug op %d", op);
 }
 
 }  // extern "C"

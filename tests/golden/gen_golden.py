@@ -440,11 +440,52 @@ def gen_ros_replay(pn, vt, out, n=120, seed=0):
                                                                 len(res['template_index']), res['templates']))
 
 
+def gen_death(pn, out):
+    """Network death: a rotation whose theta origin lies
+    beyond the 7-tap window (posecell_network.py:304-308; vrot = pi/4 at TH = 36
+    is origin floor(4.5 + .5) = 5) zeroes the whole volume; the dead steps after it
+    take the total == 0 branch (no normalisation, :343-345) and get_pc_max of an
+    all-zero volume is the first cell (:317-319); a second inject revives it.
+    Per grid: `live` normal steps, the killing step, `dead` normal steps, then
+    inject(1, revive) and `after` more normal steps."""
+    for name, shape, vrot_kill, revive in (('pc_death64', (64, 64, 36), np.pi / 4, (5, 60, 3)),
+                                           ('pc_death32', (32, 32, 18), np.pi / 2, (30, 2, 17))):
+        r = np.random.default_rng(7)
+        live, dead, after = 6, 4, 6
+        n = live + 1 + dead + after
+        odom = np.stack([r.uniform(0, 0.6, n), r.uniform(-0.15, 0.15, n)], axis=1)
+        odom[live] = (0.25, vrot_kill)
+        net = pn.PoseCellNetwork(shape)
+        loc = tuple(int(math.floor(s / 2)) for s in shape)
+        net.inject(1, loc)
+        revive_at = live + 1 + dead          # inject before this step
+        maxes, nnz, idxs, vals, totals, getmax = [], [], [], [], [], []
+        for s, v in enumerate(odom):
+            if s == revive_at:
+                net.inject(1, revive)
+            net.update((float(v[0]), float(v[1])))
+            maxes.append(net.max_pc)
+            getmax.append(net.get_pc_max())
+            i, x = coo(net.posecells)
+            nnz.append(len(i))
+            idxs.append(i)
+            vals.append(x)
+            totals.append(float(np.sum(net.posecells)))
+        assert all(nnz[s] == 0 for s in range(live, revive_at)), nnz
+        np.savez_compressed(os.path.join(out, f'{name}.npz'),
+                            shape=np.array(shape, dtype=np.int64), inject=np.array(loc, dtype=np.int64),
+                            odom=odom, max_pc=np.array(maxes, dtype=np.int64),
+                            get_pc_max=np.array(getmax, dtype=np.int64), nnz=np.array(nnz, dtype=np.int64),
+                            coo_idx=np.concatenate(idxs), coo_val=np.concatenate(vals),
+                            totals=np.array(totals), kill_step=np.int64(live),
+                            revive_step=np.int64(revive_at), revive=np.array(revive, dtype=np.int64))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default=os.path.dirname(os.path.abspath(__file__)))
     ap.add_argument('--only', choices=['kernels', 'posecell', 'templates', 'float_pairs',
-                                       'ros_replay'])
+                                       'ros_replay', 'death'])
     args = ap.parse_args()
     pn, vt = load_reference()
     if args.only in (None, 'kernels'):
@@ -457,6 +498,8 @@ def main():
         gen_float_pairs(vt, args.out)
     if args.only in (None, 'ros_replay'):
         gen_ros_replay(pn, vt, args.out)
+    if args.only in (None, 'death'):
+        gen_death(pn, args.out)
     print('golden vectors written to', args.out)
 
 

@@ -50,6 +50,26 @@ def test_posecell_trajectory_bit_exact(name):
         assert np.array_equal(net.posecells, dense_state(case, s)), (name, s)
 
 
+@pytest.mark.parametrize('name', ['pc_death64', 'pc_death32'])
+def test_network_death_bit_exact(name):
+    """The reference's network-death regime (posecell_network.py:304-308,343-345):
+    a rotation beyond the 7-tap theta window zeroes the volume, the dead steps
+    skip the normalisation (total == 0), get_pc_max of zeros is (0, 0, 0), and a
+    second inject revives the network."""
+    case = load_golden(name)
+    net = P.PoseCellOracle(tuple(case['shape']))
+    net.inject(1, tuple(case['inject']))
+    kill, revive = int(case['kill_step']), int(case['revive_step'])
+    for s, v in enumerate(case['odom']):
+        if s == revive:
+            net.inject(1, tuple(case['revive']))
+        m = net.update(v)
+        assert m == tuple(case['max_pc'][s]) == tuple(case['get_pc_max'][s]) == net.get_pc_max()
+        assert np.array_equal(net.posecells, dense_state(case, s)), (name, s)
+        if kill <= s < revive:
+            assert not net.posecells.any() and m == (0, 0, 0)
+
+
 def test_keyerror_parity():
     case = load_golden('pc_keyerror')
     assert str(case['raised']) == '(5, 5)'

@@ -42,6 +42,45 @@ def test_golden_trajectory(pcn, name, precision, tol):
     assert worst < tol, worst
 
 
+@pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
+@pytest.mark.parametrize('form', ['rows', 'cols', 'stream', 'tiles'])
+@pytest.mark.parametrize('name', ['pc_death64', 'pc_death32'])
+def test_network_death_vs_reference(pcn, monkeypatch, name, form, precision, tol):
+    """Golden fixture made by the reference (gen_golden.py --only death): a
+    rotation beyond the theta window kills the network, the dead steps take the
+    total == 0 branch (posecell_network.py:343-345) and must stay exactly zero
+    (no NaN from a 0/0), the peak of the all-zero volume is (0, 0, 0) from
+    update() and get_pc_max(), and a second inject revives it.  update() per
+    step, and run() in two batches around the second inject."""
+    monkeypatch.setenv('RS_PC_FORM', form)
+    case = load_golden(name)
+    shape = tuple(int(s) for s in case['shape'])
+    kill, revive = int(case['kill_step']), int(case['revive_step'])
+    odom = case['odom']
+    net = pcn(shape, precision=precision)
+    assert net.step_form() == form
+    net.inject(1, tuple(case['inject']))
+    for s, v in enumerate(odom):
+        if s == revive:
+            net.inject(1, tuple(int(c) for c in case['revive']))
+        m = net.update(v)
+        assert m == tuple(case['max_pc'][s]), (s, m)
+        assert net.get_pc_max() == tuple(case['get_pc_max'][s])
+        p = net.posecells
+        if kill <= s < revive:
+            assert not p.any(), s          # exactly zero, not NaN
+            net._max_valid = False
+            assert net.get_pc_max() == (0, 0, 0)   # argmax of the volume itself
+        assert np.abs(p - dense_state(case, s)).max() < tol, s
+    b = pcn(shape, precision=precision)
+    b.inject(1, tuple(case['inject']))
+    m1 = b.run(odom[:revive])
+    b.inject(1, tuple(int(c) for c in case['revive']))
+    m2 = b.run(odom[revive:])
+    assert np.array_equal(np.concatenate([m1, m2]), case['max_pc'])
+    assert np.abs(b.posecells - dense_state(case, len(odom) - 1)).max() < tol
+
+
 def test_run_equals_repeated_update(pcn):
     # 4,200 steps in one run(): more results than one pass of the export kernel's
     # grid (64 blocks x 64 steps), so its grid-stride loop is exercised
@@ -90,26 +129,96 @@ def test_mixed_shift_widths_vs_oracle(pcn, precision, tol):
         assert np.abs(net.posecells - ref.posecells).max() < tol
 
 
-def test_large_grid_properties(pcn):
-    """128x128x72 (BASELINE config 4): parity on two steps vs the oracle, then
-    size-independent properties over a long rollout: non-negative, finite,
-    float32 == float64 device paths within tolerance, argmax agreement."""
+def _own_argmax(net):
+    p = net.posecells
+    return tuple(int(v) for v in np.unravel_index(np.argmax(p), p.shape)), p
+
+
+def test_large_grid_full_rollout_vs_c_oracle(pcn):
+    """128x128x72 (BASELINE configs[3]): 40 steps of update() against the C/OpenMP
+    oracle (float64, the reference's kernels restated), float32 and float64
+    handles.  At every step the returned peak equals the oracle's AND the
+    argmax of the handle's own state (this separates the fused argmax-key path
+    from the state path), the state is finite and non-negative, and the state
+    stays within the north_star tolerance of the oracle's."""
+    from oracle import c_oracle as C
     shape = (128, 128, 72)
     od = odometry(40, 9)
     a, b = pcn(shape), pcn(shape, precision='float64')
-    ref = P.PoseCellOracle(shape)
+    assert a.step_form() == 'cols'
+    ref = C.PoseCellC(shape)
     for n in (a, b, ref):
         n.inject(1, (64, 64, 36))
-    for s in range(2):
+    for s in range(len(od)):
         m = ref.update(od[s])
-        assert a.update(od[s]) == m and b.update(od[s]) == m
-    assert np.abs(a.posecells - ref.posecells).max() < F32_TOL
-    assert np.abs(b.posecells - ref.posecells).max() < F64_TOL
-    ma, mb = a.run(od[2:]), b.run(od[2:])
-    assert np.array_equal(ma, mb)
-    pa, pb = a.posecells, b.posecells
-    assert np.isfinite(pa).all() and (pa >= 0).all()
-    assert np.abs(pa - pb).max() < F32_TOL
+        for net, tol in ((a, F32_TOL), (b, F64_TOL)):
+            got = net.update(od[s])
+            own, p = _own_argmax(net)
+            assert got == own, (net.precision, s, got, own)
+            assert got == m, (net.precision, s, got, m)
+            assert np.isfinite(p).all() and (p >= 0).all()
+            err = np.abs(p - ref.posecells).max()
+            assert err < tol, (net.precision, s, err)
+    # batched form: the same trajectory through run() on fresh handles
+    c = pcn(shape)
+    c.inject(1, (64, 64, 36))
+    ref2 = C.PoseCellC(shape)
+    ref2.inject(1, (64, 64, 36))
+    mc = c.run(od)
+    assert [tuple(r) for r in mc] == [ref2.update(v) for v in od]
+    assert np.abs(c.posecells - ref2.posecells).max() < F32_TOL
+
+
+# every step form on a fresh handle whose scratch is poisoned (rs_pc_debug): a
+# step that read an excited cell, a partial sum or an argmax slot it had not
+# written in that step would give NaN state or a wrong peak, every time
+POISON_CASES = [((128, 128, 72), 'cols'), ((128, 128, 100), 'cols'), ((64, 64, 36), 'rows'),
+                ((40, 44, 20), 'tiles'), ((128, 130, 72), 'stream')]
+
+
+@pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
+@pytest.mark.parametrize('shape,form', POISON_CASES)
+def test_poisoned_scratch_first_updates_vs_c_oracle(pcn, monkeypatch, shape, form, precision, tol):
+    from oracle import c_oracle as C
+    from pyratslam_amd import _lib
+    monkeypatch.setenv('RS_PC_FORM', form)
+    od = odometry(4, 31)
+    loc = tuple(s // 2 for s in shape)
+    ref = C.PoseCellC(shape)
+    ref.inject(1, loc)
+    want = [ref.update(v) for v in od]
+    for batched in (False, True):
+        net = pcn(shape, precision=precision)
+        assert net.step_form() == form
+        _lib.check(net._lib.rs_pc_debug(net._h, _lib.RS_PC_DBG_POISON))
+        net.inject(1, loc)
+        got = [tuple(r) for r in net.run(od)] if batched else [net.update(v) for v in od]
+        assert got == want, (shape, form, precision, batched)
+        p = net.posecells
+        assert np.isfinite(p).all()
+        assert np.abs(p - ref.posecells).max() < tol
+        net.close()
+
+
+def test_result_export_sentinel(pcn):
+    """A step whose argmax key never reaches the host result word fails loudly
+    (rs_pc_debug(RS_PC_DBG_SKIP_EXPORT) withholds the export once); the next
+    update is correct."""
+    from pyratslam_amd import _lib
+    shape = (32, 32, 18)
+    net = pcn(shape)
+    ref = P.PoseCellOracle(shape)
+    for n in (net, ref):
+        n.inject(1, (16, 16, 9))
+    od = odometry(3, 2)
+    _lib.check(net._lib.rs_pc_debug(net._h, _lib.RS_PC_DBG_SKIP_EXPORT))
+    with pytest.raises(_lib.HipLibraryError, match='did not reach'):
+        net.update(od[0])
+    ref.update(od[0])                  # the step itself ran
+    assert net.update(od[1]) == ref.update(od[1])
+    assert net.run(od[2:]).tolist() == [list(ref.update(od[2]))]
+    with pytest.raises(ValueError):
+        _lib.check(net._lib.rs_pc_debug(net._h, 99))
 
 
 @pytest.mark.parametrize('form', ['', 'cols'])   # cols: P theta-fastest, Q layer-major
