@@ -89,30 +89,11 @@ __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
     return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
 }
 
-// Phase stamps for the diagnostic probe (tools/pc_probe.hip defines PC_STAMPS);
-// compiled out of the library.
-#ifdef PC_STAMPS
-#define PC_STAMP(kid, sid)                                                              \
-    do {                                                                                \
-        if (threadIdx.x == 0) {                                                         \
-            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                    \
-            pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memrealtime(); \
-        }                                                                               \
-    } while (0)
-// shader-clock stamp (s_memtime) of thread 0, for per-phase cycle counts
-#define PC_STAMPC(kid, sid)                                                             \
-    do {                                                                                \
-        if (threadIdx.x == 0) {                                                         \
-            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                    \
-            pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memtime();     \
-        }                                                                               \
-    } while (0)
-#else
+// Phase-stamp hooks, empty in the library.  tools/pc_probe.hip defines them (a
+// per-block s_memrealtime stamp) before it includes this file.
+#ifndef PC_STAMP
 #define PC_STAMP(kid, sid) \
     do {                   \
-    } while (0)
-#define PC_STAMPC(kid, sid) \
-    do {                    \
     } while (0)
 #endif
 
@@ -365,12 +346,7 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
 // 2 x 4 (8 waves) made 288 blocks, and the CUs that ran two of them set the
 // kernels' span (path 8.7 -> 5.2 us, excitation 4.6 -> 3.8 us first block start
 // to last block end; it also re-evaluates fewer halo rows and layers per output).
-// -D overrides for A/B builds of tools/pc_probe.hip.
-#ifndef PC_RT_BX
-#define PC_RT_BX 2
-#define PC_RT_BK 6
-#endif
-constexpr int RT_BX = PC_RT_BX, RT_BK = PC_RT_BK, RT_NW = RT_BK + 6, RT_NT = 64 * RT_NW;
+constexpr int RT_BX = 2, RT_BK = 6, RT_NW = RT_BK + 6, RT_NT = 64 * RT_NW;
 constexpr int RT_NFMAX = 8;  // filter tables up to this size are preloaded whole
 
 template <int NW>
@@ -761,16 +737,11 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 // XCD x takes a contiguous run of tiles, so neighbouring tiles' halo rows and
 // layers meet in the same L2.
 // ---------------------------------------------------------------------------
-#ifndef PC_ST_PF
-#define PC_ST_PF 3
-#endif
-constexpr int ST_PF = PC_ST_PF;           // window prefetch distance (layers)
+constexpr int ST_PF = 3;                  // window prefetch distance (layers)
 // The streaming grids hold 1-2 blocks per CU, so occupancy buys nothing: let the
 // scheduler spend registers on keeping LDS reads in flight (at the default
 // occupancy target it serialises every ds_read behind an lgkmcnt(0)).
-#ifndef PC_ST_WAVES
 #define PC_ST_WAVES __attribute__((amdgpu_waves_per_eu(1, 2)))
-#endif
 constexpr int ST_MAXKC = 12;              // layers per block (outputs buffered in LDS)
 constexpr int ST_MAXL = ST_MAXKC + 2 * 3 + ST_PF + 1;  // control entries staged in LDS
 constexpr int ST_OUT_BYTES = 24 * 1024;   // LDS output buffer per block
@@ -800,9 +771,6 @@ __device__ inline int st_tile(int b, int nb) {
 // fault with two processes on one GPU; the plain form measures within 2%.)
 template <typename T>
 __device__ inline T st_load(const T* base, unsigned idx) {
-#ifdef PC_DIAG_NOLOAD  // diagnostic build of tools/pc_probe.hip only: no window traffic
-    return (T)(idx & 7) * (T)1e-3;
-#endif
     return base[idx];
 }
 
@@ -1173,23 +1141,12 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 // Window rows/cols wrap with one conditional add/subtract, so X >= TX+6 and
 // Y >= TY+6 (checked on the host); TH <= co_thmax (the window in LDS).
 // ---------------------------------------------------------------------------
-#ifndef PC_CO_NW
-#define PC_CO_NW 12  // 9, 10, 11, 13, 14, 16: 20.6, 20.3, 20.2, 20.5, 20.3, 20.2 us vs 19.8 at 128x128x72
-#endif
-#ifndef PC_CO_TX
-#define PC_CO_TX 8
-#endif
-#ifndef PC_CO_FSPLIT
-#define PC_CO_FSPLIT 2  // 7x7 filter tasks per output column
-#endif
-#ifndef PC_CO_FROWS
-#define PC_CO_FROWS 2   // 7x7 filter: window rows scheduled together
-#endif
-#ifndef PC_CO_FCOLS
-#define PC_CO_FCOLS 2   // 7x7 filter: output columns per task
-#endif
-// 12 waves per block (768 threads; -D overrides for A/B builds of the probe)
-constexpr int CO_TX = PC_CO_TX, CO_TY = 8, CO_NW = PC_CO_NW;
+// 12 waves per block (768 threads; 9, 10, 11, 13, 14, 16: 20.6, 20.3, 20.2, 20.5,
+// 20.3, 20.2 us vs 19.8 per 128x128x72 step)
+constexpr int CO_TX = 8, CO_TY = 8, CO_NW = 12;
+// 7x7 filter tasks of the path kernel: 2 tasks per output column (4-row halves),
+// 2 output columns per task, window rows scheduled 2 at a time
+constexpr int CO_FSPLIT = 2, CO_FCOLS = 2, CO_FROWS = 2;
 constexpr int CO_CH = 8;                        // layers per theta-pass task (scalar stream/rows helpers)
 constexpr int CO_TCL = 2;                       // column theta passes: output layers per task
 constexpr int CO_LDS = 150 * 1024;              // LDS budget of the excitation kernel
@@ -1501,9 +1458,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
 #pragma unroll
                 for (int c = 0; c < VEC; ++c) qv[c] = (v[c] < k.inhib) ? T(0) : v[c] - k.inhib;
                 if (mine && lo < ly.nout) {
-#ifndef PC_DIAG_NOSTORE
                     co_put(Q, ((size_t)gk * X + gi) * Y + gy, qv, wt, nbytes);
-#endif
 #pragma unroll
                     for (int c = 0; c < VEC; ++c) sum += (double)qv[c];
                 }
@@ -1604,9 +1559,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     PC_STAMP(6, 2);
     // 7x7 filter: task (L, column group, row part) -> TX/FS rows x CP columns of
     // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each
-    // window row's reads; reads of PC_CO_FROWS rows at a time in flight: hoisting all
+    // window row's reads; reads of CO_FROWS rows at a time in flight: hoisting all
     // of them spills at 3 waves per SIMD)
-    constexpr int FS = PC_CO_FSPLIT, TXH = TX / FS, CP = PC_CO_FCOLS, NCG = TY / CP;
+    constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
     {
         for (int t = tid; t < ly.nl * NCG * FS; t += NT) {
@@ -1624,7 +1579,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                 T w[FL + CP - 1];
 #pragma unroll
                 for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[a * RP + q];
-                if (a % PC_CO_FROWS == PC_CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
+                if (a % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < TXH; ++i) {
                     const int x = a - i;
@@ -1698,7 +1653,6 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
             if (gi < X && gy < Y) {
                 const int gk0 = ly.k0 + j * VEC, nv = min(VEC, ly.nout - j * VEC);
                 const size_t e0 = ((size_t)gi * Y + gy) * TH + gk0;
-#ifndef PC_DIAG_NOSTORE
                 if (nv == VEC && e0 % VEC == 0) {
                     co_put(P, e0, v, wt, nbytes);
                 } else {  // a ragged or unaligned group (TH or the chunk not a multiple of VEC)
@@ -1706,7 +1660,6 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                     for (int o = 0; o < VEC; ++o)
                         if (o < nv) P[e0 + o] = v[o];
                 }
-#endif
 #pragma unroll
                 for (int o = 0; o < VEC; ++o) {
                     if (o >= nv) break;
@@ -2111,7 +2064,7 @@ PcCtlRing make_ctl_ring(const rs_pc* h, int s) {
 }
 
 // Streaming variants instantiated: (BX rows per wave, WR row groups, WC column tiles of 64).
-#define PC_STREAM_VARIANTS(X_) X_(1, 8, 1) X_(2, 8, 1) X_(1, 4, 2) X_(2, 4, 2)
+#define PC_STREAM_VARIANTS(X_) X_(1, 8, 1) X_(2, 8, 1)
 
 template <typename T, typename CTL>
 int pc_launch_stream(rs_pc* h, const T* P, T* Q, unsigned long long* slot, T* bmax, unsigned* bidx,

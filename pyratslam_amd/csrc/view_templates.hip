@@ -364,30 +364,14 @@ __global__ __launch_bounds__(64) void vt_scan_generic_kernel(const uint4* __rest
 // ===========================================================================
 constexpr int PL_CG = 4;       // column groups of 8 bytes: W = 32
 
-// Per-wave start/end stamps for the diagnostic probe (tools/vt_probe.hip defines
-// VT_STAMPS and the vt_dbg buffer): realtime (100 MHz), shader clock, hw ids.
-#ifdef VT_STAMPS
-#define VT_STAMP(slot)                                                                     \
-    do {                                                                                   \
-        if ((threadIdx.x & 63) == 0) {                                                     \
-            unsigned hw_, xcc_;                                                            \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
-            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6; \
-            d_[(slot) * 3 + 0] = __builtin_amdgcn_s_memrealtime();                         \
-            d_[(slot) * 3 + 1] = __builtin_amdgcn_s_memtime();                             \
-            d_[(slot) * 3 + 2] = ((unsigned long long)xcc_ << 32) | hw_;                   \
-        }                                                                                  \
-    } while (0)
-#else
+// Per-wave stamp hook, empty in the library: tools/vt_probe.hip defines it (start
+// and end of every wave: realtime, shader clock, hw ids) before it includes this file.
+#ifndef VT_STAMP
 #define VT_STAMP(slot) \
     do {               \
     } while (0)
 #endif
-#ifndef PL_NB_Q
-#define PL_NB_Q 4
-#endif
-constexpr int PL_NB = PL_NB_Q;  // queries per LDS batch (staged planes; one reducing wave each)
+constexpr int PL_NB = 4;  // queries per LDS batch (staged planes; one reducing wave each)
 
 // One block per stored template: planes + TS of raw template src[t] into slot dst[t].
 __global__ __launch_bounds__(256) void vt_plane_store_kernel(const uint8_t* __restrict__ raw,
@@ -566,14 +550,35 @@ struct PlaneLds {
     static constexpr int M = FAST_M, NS = H - 2 * M + 3, NO = 2 * M - 1, NK = (NO + 1) / 2;
     static constexpr int QW = PL_CG * NS * 8;                 // query-plane dwords per query
     static constexpr int NW = PL_CG * PL_SPLIT;                // waves per block
-    // double-buffered: batch i computes from q[i&1] and adds its partial counts into
-    // part[i&1] while batch i+1 is staged into q[(i+1)&1]; one barrier per batch
     static constexpr int QP = (PL_NB * QW / 4 + 63) / 64 * 64;  // padded to whole 1 KiB wave-instructions
-    uint4 q[2][QP];
-    uint32_t part[2][PL_NB][NK][64];                           // u16 pairs, summed by ds_add
-    int bidx[3];                                               // batches taken ahead (ring)
-    uint32_t ts[16][64];                                       // TS(o) of the 64 templates
 };
+
+// The plane scan's LDS.  Double-buffered: batch i computes from its staged query
+// planes and adds its partial counts into part[i&1] while batch i+1 is staged into
+// the other plane buffer; one barrier per batch.  Each buffer is its own
+// namespace-scope __shared__ variable and every access names one of them at
+// compile time (pl_q<CUR>, pl_part<CUR>): hipcc waits for an LDS-DMA in flight
+// before any LDS access it cannot prove disjoint from the DMA's variable, so
+// only distinct, statically named variables let the next batch's DMA stay in
+// flight through this batch's compute.
+constexpr int PL_NK = PlaneLds<64>::NK;
+constexpr int PL_QP = PlaneLds<64>::QP;   // H = 64 is the larger instantiation
+__shared__ uint4 vt_pl_qa[PL_QP];         // staged query planes, even batches
+__shared__ uint4 vt_pl_qb[PL_QP];         // odd batches
+__shared__ uint32_t vt_pl_part0[PL_NB][PL_NK][64];  // u16 pairs of partial counts, summed by ds_add
+__shared__ uint32_t vt_pl_part1[PL_NB][PL_NK][64];
+__shared__ int vt_pl_bidx[3];             // batches taken ahead (ring)
+__shared__ uint32_t vt_pl_ts[16][64];     // TS(o) of the block's 64 templates
+template <int CUR>
+__device__ __forceinline__ uint4* pl_q() {
+    if constexpr (CUR == 0) return vt_pl_qa;
+    else return vt_pl_qb;
+}
+template <int CUR>
+__device__ __forceinline__ uint32_t (&pl_part())[PL_NB][PL_NK][64] {
+    if constexpr (CUR == 0) return vt_pl_part0;
+    else return vt_pl_part1;
+}
 
 template <int H, int HALF>
 __device__ __forceinline__ void plane_load_units(const uint4* __restrict__ planes, int tb, int cg,
@@ -595,77 +600,115 @@ __device__ __forceinline__ void plane_load_units(const uint4* __restrict__ plane
 // finishes query w of the batch and clears its partial slots for batch i+2.
 // Batches are taken one ahead by thread 0; a block stops taking after its first
 // failed take, so every block ends on exactly one failed take (counter rewind).
+// One batch of plane_wave: compute from qcur (staged by the previous batch or the
+// prologue) while this wave's share of the next batch goes global -> LDS into qnxt.
+// CUR is the parity of the iteration (it & 1), so the plane buffers and the
+// partial-count slots are compile-time: each LDS read names one __shared__
+// variable and each DMA the other, and hipcc leaves the DMA in flight through the
+// compute (a runtime choice of buffer made it wait vmcnt(0) before the first read).
+// Returns false once the block has no batch left.
+template <int H, int HALF, bool MATRIX, int CUR>
+__device__ __forceinline__ bool plane_batch(const uint32_t (&P)[PlaneRange<H, HALF>::NUH][8], int it,
+                                            int& bi, int nbatch, int64_t slot, int64_t count,
+                                            const uint4* __restrict__ qp4, const uint32_t* __restrict__ qsum,
+                                            int nq, unsigned* __restrict__ ctr, int G, int g, ScanOut out,
+                                            int rank, int nranks, int wave, int cg, int lane,
+                                            unsigned& failed) {
+    using R = PlaneRange<H, HALF>;
+    using LD = PlaneLds<H>;
+    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
+    if (bi >= nbatch) return false;  // block-uniform
+    const uint4* qcur = pl_q<CUR>();
+    uint4* qnxt = pl_q<CUR ^ 1>();
+    uint32_t(&part)[PL_NB][PL_NK][64] = pl_part<CUR>();
+    const int tid = wave * 64 + lane;
+    // batch ring: iteration it reads the next batch from slot (it+1) % 3 and thread
+    // 0 writes the one after it into slot (it+2) % 3, last read two barriers ago
+    const int r1 = (it + 1) % 3, r2 = (it + 2) % 3;
+    const int bn = vt_pl_bidx[r1];
+    const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
+    // The take comes first (its result is waited for); with no next batch there is
+    // no further take: this block's failed take was bn.
+    if (tid == 0) {  // the batch after next
+        const unsigned t = bn < nbatch ? atomicAdd(ctr, 1u) : (unsigned)nbatch;
+        vt_pl_bidx[r2] = (int)t;
+        if (bn < nbatch && (int)t >= nbatch) failed = t;
+    }
+    // the next batch's planes go global -> LDS directly (global_load_lds, 1 KiB per
+    // wave-instruction, lane-linear), in flight through this batch's compute
+    if (bn < nbatch) {
+        const int qn = (bn * G + g) * PL_NB, nbn = min(PL_NB, nq - qn);
+        const int lim = nbn * LD::QW / 4;
+        const uint4* src = qp4 + (size_t)qn * (LD::QW / 4);
+#pragma unroll
+        for (int k = 0; k < (LD::QP + NT - 1) / NT; ++k) {
+            const int i0 = wave * 64 + k * NT;  // wave-uniform
+            if (i0 < lim)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) const void*)(src + min(i0 + lane, lim - 1)),
+                    (__attribute__((address_space(3))) void*)(qnxt + i0), 16, 0, 0);
+        }
+    }
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        uint32_t acc[NO];
+#pragma unroll
+        for (int o = 0; o < NO; ++o) acc[o] = 0u;
+        plane_rows<H, HALF, R::SA>(P, reinterpret_cast<const uint32_t*>(qcur) + (b * PL_CG + cg) * NS * 8, acc);
+#pragma unroll
+        for (int k = 0; k < NK; ++k)
+            atomicAdd(&part[b][k][lane], acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u));
+    }
+    // every wave's DMA into qnxt has landed before any wave passes the barrier and
+    // reads it (explicit: nothing else guarantees this wait stays in front of it)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    if (wave < nb) {  // wave w finishes query qb + w of the batch
+        const int qi = qb + wave;
+        uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const uint32_t t = part[wave][k][lane];
+            part[wave][k][lane] = 0u;
+            best = min(best, vt_pl_ts[2 * k][lane] + 256u * (t & 0xFFFFu));
+            if (2 * k + 1 < NO) best = min(best, vt_pl_ts[2 * k + 1][lane] + 256u * (t >> 16));
+        }
+        emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
+    }
+    bi = bn;
+    return true;
+}
+
 template <int H, int HALF, bool MATRIX>
-__device__ __forceinline__ void plane_wave(PlaneLds<H>& L, const uint4* __restrict__ planes,
+__device__ __forceinline__ void plane_wave(const uint4* __restrict__ planes,
                                            int tb, int64_t count, const uint4* __restrict__ qp4,
                                            const uint32_t* __restrict__ qsum, int nq,
                                            unsigned* __restrict__ ctr, int G, int g, ScanOut out,
                                            int rank, int nranks, int wave, int cg, int lane,
                                            unsigned& failed) {
     using R = PlaneRange<H, HALF>;
-    using LD = PlaneLds<H>;
-    constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
     uint32_t P[R::NUH][8];
     plane_load_units<H, HALF>(planes, tb, cg, lane, P);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the template planes have landed before the loop
     const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
     const int64_t slot = (int64_t)tb * 64 + lane;
-    const int tid = wave * 64 + lane;
-    // batch ring: iteration it reads the next batch from slot (it+1) % 3 and thread
-    // 0 writes the one after it into slot (it+2) % 3, last read two barriers ago
-    int bi = L.bidx[0];
-    for (int it = 0;; ++it) {
-        if (bi >= nbatch) break;  // block-uniform
-        const int cur = it & 1, nxt = cur ^ 1, r1 = (it + 1) % 3, r2 = (it + 2) % 3;
-        const int bn = L.bidx[r1];
-        const int qb = (bi * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
-        // the next batch's planes go global -> LDS directly (global_load_lds, 1 KiB per
-        // wave-instruction, lane-linear), in flight through this batch's compute; the
-        // barrier's vmcnt(0) retires them.  The take comes first (its result is waited for);
-        // with no next batch there is no further take: this block's failed take was bn.
-        if (tid == 0) {  // the batch after next
-            const unsigned t = bn < nbatch ? atomicAdd(ctr, 1u) : (unsigned)nbatch;
-            L.bidx[r2] = (int)t;
-            if (bn < nbatch && (int)t >= nbatch) failed = t;
-        }
-        if (bn < nbatch) {
-            const int qn = (bn * G + g) * PL_NB, nbn = min(PL_NB, nq - qn);
-            const int lim = nbn * LD::QW / 4;
-            const uint4* src = qp4 + (size_t)qn * (LD::QW / 4);
-#pragma unroll
-            for (int k = 0; k < (LD::QP + NT - 1) / NT; ++k) {
-                const int i0 = wave * 64 + k * NT;  // wave-uniform
-                if (i0 < lim)
-                    __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) const void*)(src + min(i0 + lane, lim - 1)),
-                        (__attribute__((address_space(3))) void*)(&L.q[nxt][i0]), 16, 0, 0);
-            }
-        }
-#pragma unroll 1
-        for (int b = 0; b < nb; ++b) {
-            uint32_t acc[NO];
-#pragma unroll
-            for (int o = 0; o < NO; ++o) acc[o] = 0u;
-            plane_rows<H, HALF, R::SA>(
-                P, reinterpret_cast<const uint32_t*>(L.q[cur]) + (b * PL_CG + cg) * NS * 8, acc);
-#pragma unroll
-            for (int k = 0; k < NK; ++k)
-                atomicAdd(&L.part[cur][b][k][lane], acc[2 * k] | (2 * k + 1 < NO ? acc[2 * k + 1] << 16 : 0u));
-        }
-        __syncthreads();
-        if (wave < nb) {  // wave w finishes query qb + w of the batch
-            const int qi = qb + wave;
-            uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-            for (int k = 0; k < NK; ++k) {
-                const uint32_t t = L.part[cur][wave][k][lane];
-                L.part[cur][wave][k][lane] = 0u;
-                best = min(best, L.ts[2 * k][lane] + 256u * (t & 0xFFFFu));
-                if (2 * k + 1 < NO) best = min(best, L.ts[2 * k + 1][lane] + 256u * (t >> 16));
-            }
-            emit_score<MATRIX>(out, slot, count, qi, nq, best - qsum[qi], rank, nranks, lane == 0);
-        }
-        bi = bn;
+    int bi = vt_pl_bidx[0];
+    // unrolled by two: even iterations compute from qa and stage into qb, odd ones
+    // the other way round (the prologue staged the first batch into qa)
+    // The first batch is peeled off the loop: hipcc's wait analysis is exact for the
+    // LDS accesses after a DMA issued in the same loop iteration but not across the
+    // loop header's merge, so the loop body starts with an odd batch, whose compute
+    // follows its own DMA issue, not the header.
+    if (!plane_batch<H, HALF, MATRIX, 0>(P, 0, bi, nbatch, slot, count, qp4, qsum, nq, ctr, G, g, out, rank,
+                                         nranks, wave, cg, lane, failed))
+        return;
+    for (int it = 1;; it += 2) {
+        if (!plane_batch<H, HALF, MATRIX, 1>(P, it, bi, nbatch, slot, count, qp4, qsum, nq, ctr, G, g, out,
+                                             rank, nranks, wave, cg, lane, failed))
+            break;
+        if (!plane_batch<H, HALF, MATRIX, 0>(P, it + 1, bi, nbatch, slot, count, qp4, qsum, nq, ctr, G, g,
+                                             out, rank, nranks, wave, cg, lane, failed))
+            break;
     }
 }
 
@@ -679,7 +722,6 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
                           const uint32_t* __restrict__ qsum, int nq, int nqc,
                           unsigned* __restrict__ next_batch, ScanOut out, int rank, int nranks) {
     static_assert(PL_SPLIT == 2, "two row ranges");
-    __shared__ PlaneLds<H> L;
     // The nqc blocks of a template block are adjacent block ids, so they are dispatched
     // together and split its query batches dynamically even when the grid runs in
     // several rounds.  XCD-aware: blocks b and b+8 share an XCD (and its L2); with
@@ -692,10 +734,12 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63, cg = wave % PL_CG, half = wave / PL_CG;
     const int nbatch = ((nq + PL_NB - 1) / PL_NB - g + G - 1) / G;
-    for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) L.ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
+    for (int i = threadIdx.x; i < 16 * 64; i += blockDim.x) vt_pl_ts[i >> 6][i & 63] = tsum[(size_t)tb * 1024 + i];
     unsigned failed = 0u;  // thread 0: the value of this block's one failed take
-    for (int i = threadIdx.x; i < 2 * PL_NB * PlaneLds<H>::NK * 64; i += blockDim.x)
-        (&L.part[0][0][0][0])[i] = 0u;
+    for (int i = threadIdx.x; i < PL_NB * PL_NK * 64; i += blockDim.x) {
+        (&vt_pl_part0[0][0][0])[i] = 0u;
+        (&vt_pl_part1[0][0][0])[i] = 0u;
+    }
     if (threadIdx.x == 0) {  // the first batch and the one after it
         const unsigned a = atomicAdd(ctr, 1u);
         unsigned b = (unsigned)nbatch;
@@ -705,23 +749,23 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
         } else {
             failed = a;
         }
-        L.bidx[0] = (int)a;
-        L.bidx[1] = (int)b;
+        vt_pl_bidx[0] = (int)a;
+        vt_pl_bidx[1] = (int)b;
     }
     __syncthreads();
-    if (L.bidx[0] < nbatch) {  // stage the first batch
+    if (vt_pl_bidx[0] < nbatch) {  // stage the first batch
         constexpr int QW4 = PlaneLds<H>::QW / 4;
-        const int qb = (L.bidx[0] * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
+        const int qb = (vt_pl_bidx[0] * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
         const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
-        for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) L.q[0][i] = qp4[(size_t)qb * QW4 + i];
+        for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) vt_pl_qa[i] = qp4[(size_t)qb * QW4 + i];
     }
     __syncthreads();
     const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
     if (half == 0)
-        plane_wave<H, 0, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
+        plane_wave<H, 0, MATRIX>(planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
                                  wave, cg, lane, failed);
     else
-        plane_wave<H, 1, MATRIX>(L, planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
+        plane_wave<H, 1, MATRIX>(planes, tb, count, qp4, qsum, nq, ctr, G, g, out, rank, nranks,
                                  wave, cg, lane, failed);
     // Each of the nqc / G blocks sharing a counter ends on exactly one failed take, so
     // the block whose failed take returned (group batches) + nqc / G - 1 is the

@@ -91,7 +91,10 @@ class Dist:
         token = secrets.token_hex(16)
         self._path = rendezvous_path()
         tmp = self._path + '.%d.tmp' % os.getpid()
-        with open(tmp, 'w') as f:
+        # owner-only from creation: the file holds the job's auth token (a file left
+        # world-readable in a shared tempdir would let another local user join)
+        fd = os.open(tmp, os.O_CREAT | os.O_EXCL | os.O_WRONLY, 0o600)
+        with os.fdopen(fd, 'w') as f:
             f.write('%d %s\n' % (srv.getsockname()[1], token))
         os.replace(tmp, self._path)
         try:

@@ -193,8 +193,16 @@ class ViewTemplates:
         _lib.check(self._lib.rs_vt_count(self._h, ctypes.byref(c)))
         return c.value
 
+    def _refuse_float(self, what):
+        # after a float frame the Python template list holds templates the device
+        # library does not (the float path scores pair-wise on the host's list)
+        if self._float:
+            raise TypeError('this library has matched float frames: %s works on uint8 '
+                            'device libraries only; use match() / match_batch()' % what)
+
     def add(self, templates, locations=None):
         """Append templates unconditionally (indices len .. len+n-1)."""
+        self._refuse_float('add()')
         t = self._check_templates(templates)
         first = ctypes.c_int64()
         with self._mutex:
@@ -208,6 +216,7 @@ class ViewTemplates:
 
     def scores(self, queries, t0=0, nt=None):
         """uint64 (nq, nt) scores of queries vs templates [t0, t0+nt) -- ViewTemplate.match."""
+        self._refuse_float('scores()')
         q = self._check_templates(queries)
         nt = self.count() - t0 if nt is None else nt
         out = np.empty((q.shape[0], nt), dtype=np.uint64)
@@ -228,9 +237,8 @@ class ViewTemplates:
 
     def match_templates(self, queries, pcs=None, mode=_lib.RS_VT_SEQUENTIAL):
         """Match already-subsampled (nq, H, W) queries; returns (index, score, is_new)."""
+        self._refuse_float('match_templates()')
         q = self._check_templates(queries)
-        if self._float:
-            raise TypeError('this library has matched float frames: use match() / match_batch()')
         n = q.shape[0]
         idx = np.empty(n, dtype=np.int64)
         score = np.empty(n, dtype=np.uint64)
@@ -248,6 +256,7 @@ class ViewTemplates:
         (rs_vt_match_stream): ``queries`` is a uint8 (nb, nq, H, W) host array, or
         ``(nb, nq, _lib.DeviceBuffer)`` for batches already in HBM.  Returns
         ``(index, score)`` shaped (nb, nq); nothing is appended."""
+        self._refuse_float('match_stream()')
         if isinstance(queries, tuple):
             nb, nq, buf = int(queries[0]), int(queries[1]), queries[2]
             if nb * nq * self.shape[0] * self.shape[1] > buf.nbytes:
@@ -335,6 +344,7 @@ class ViewTemplates:
         ``(n, _lib.DeviceBuffer)`` (n whole frames back to back), gathered in
         place.  Returns ``(index, score, is_new)`` like ``match_templates``.
         """
+        self._refuse_float('match_frames()')
         self._ensure_gather()
         dev = isinstance(frames, tuple)
         if dev:

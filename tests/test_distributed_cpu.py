@@ -120,3 +120,40 @@ def test_bench_spawns_its_own_ranks(monkeypatch):
     assert e.value.code == 0
     assert seen['n'] == 4 and seen['argv'][0].endswith('bench.py') and seen['argv'][1:] == [
         '--gpus', '4', '--steps', '3']
+
+
+def test_rendezvous_file_is_owner_only(tmp_path, monkeypatch):
+    """The rendezvous file holds the job's auth token: rank 0 creates it 0600
+    (a world-readable file in a shared tempdir would let another local user join)."""
+    import stat
+    import threading
+    from pyratslam_amd import dist
+    monkeypatch.setenv('RS_DIST_DIR', str(tmp_path))
+    monkeypatch.setenv('WORLD_SIZE', '2')
+    monkeypatch.setenv('RANK', '0')
+    monkeypatch.setenv('MASTER_ADDR', '127.0.0.1')
+    seen = {}
+    path = dist.rendezvous_path()
+
+    def watch():
+        import time
+        t_end = time.monotonic() + 20
+        while time.monotonic() < t_end and not os.path.exists(path):
+            time.sleep(0.01)
+        seen['mode'] = stat.S_IMODE(os.stat(path).st_mode)
+        port, token = open(path).read().split()
+        import socket
+        s = socket.create_connection(('127.0.0.1', int(port)))
+        dist._send(s, ('%s 1' % token).encode())
+        seen['ack'] = dist._recv(s)
+        seen['sock'] = s
+
+    t = threading.Thread(target=watch)
+    t.start()
+    d = dist.Dist(timeout=20)
+    t.join()
+    assert seen['mode'] == 0o600
+    assert seen['ack'] == b'ok'
+    seen['sock'].close()
+    for c in d._peers.values():
+        c.close()

@@ -325,6 +325,12 @@ def test_float_frames_trace(vtmod):
         t = vts.match(_float_frame(vts.mask, q), k % 21, (3 * k) % 21, (5 * k) % 36)
         assert t.get_index() == d['trace_index'][k]
     assert np.array_equal(np.stack([t.template for t in vts.templates]), d['trace_templates'])
+    # the device library no longer mirrors the template list: its calls refuse
+    u8 = np.zeros((1,) + vts.shape, dtype=np.uint8)
+    for call in (lambda: vts.add(u8), lambda: vts.scores(u8), lambda: vts.match_templates(u8),
+                 lambda: vts.match_stream(u8[None])):
+        with pytest.raises(TypeError, match='float frames'):
+            call()
 
 
 def _float_frame(mask, template):

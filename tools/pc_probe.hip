@@ -1,5 +1,5 @@
 // Diagnostic probe for the pose-cell step kernels (not part of the library).
-// Builds posecell.hip with PC_STAMPS so the row kernels write s_memrealtime
+// Builds posecell.hip with its PC_STAMP hook defined so the step kernels write s_memrealtime
 // stamps (100 MHz) at their phase boundaries, then reports per-phase times
 // over the blocks of one step, and back-to-back launch costs of each kernel
 // alone and of an empty kernel with the same grid.
@@ -12,8 +12,15 @@
 #include <cstdio>
 #include <vector>
 
-#define PC_STAMPS 1
+// the library's phase-stamp hook (posecell.hip leaves it empty)
 __device__ unsigned long long* pc_dbg;
+#define PC_STAMP(kid, sid)                                                              \
+    do {                                                                                \
+        if (threadIdx.x == 0) {                                                         \
+            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x;                    \
+            pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                               \
+    } while (0)
 #include "posecell.hip"
 
 #define CK(x)                                                                  \

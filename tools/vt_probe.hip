@@ -1,5 +1,5 @@
 // Diagnostic probe for the bit-plane template scan (not part of the library).
-// Builds view_templates.hip with VT_STAMPS so every wave of vt_scan_plane_kernel
+// Builds view_templates.hip with its VT_STAMP hook defined so every wave of vt_scan_plane_kernel
 // stamps its start and end (realtime 100 MHz, shader clock, hw ids), then
 // reports the kernel span, wave durations, waves per SIMD and the clock.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ipyratslam_amd/csrc \
@@ -13,8 +13,20 @@
 #include <random>
 #include <vector>
 
-#define VT_STAMPS 1
+// the library's per-wave stamp hook (view_templates.hip leaves it empty)
 __device__ unsigned long long* vt_dbg;
+#define VT_STAMP(slot)                                                                     \
+    do {                                                                                   \
+        if ((threadIdx.x & 63) == 0) {                                                     \
+            unsigned hw_, xcc_;                                                            \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));              \
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));            \
+            unsigned long long* d_ = vt_dbg + ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 6; \
+            d_[(slot) * 3 + 0] = __builtin_amdgcn_s_memrealtime();                         \
+            d_[(slot) * 3 + 1] = __builtin_amdgcn_s_memtime();                             \
+            d_[(slot) * 3 + 2] = ((unsigned long long)xcc_ << 32) | hw_;                   \
+        }                                                                                  \
+    } while (0)
 #include "view_templates.hip"
 
 int main(int argc, char** argv) {
