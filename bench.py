@@ -75,6 +75,8 @@ def parse():
                     help='timed pose-cell steps (SURVEY.md 8(d): >= 10,000)')
     ap.add_argument('--pc-warmup', type=int, default=200)
     ap.add_argument('--pc-calls', type=int, default=10000, help='timed per-call update()s')
+    ap.add_argument('--node-calls', type=int, default=2000,
+                    help='timed update() + .posecells read pairs (the ROS node step)')
     ap.add_argument('--pc-stress-shape', default='128,128,72',
                     help='configs[3] stencil-stress grid, reported beside the headline grid')
     ap.add_argument('--pc-stress-steps', type=int, default=10000)
@@ -397,6 +399,44 @@ def bench_posecells(args, d):
     }
 
 
+def bench_node_step(args, d):
+    """The ROS node's per-step drop-in cost (ros_simulate.py:134-145): update()
+    and then a read of the whole ``.posecells`` volume (the node publishes it as a
+    Float64MultiArray after every step), per call, at the node's grid (21x21x36,
+    ros_simulate.py:31) and the headline grid."""
+    from pyratslam_amd import PoseCellNetwork, synthetic
+    out = {}
+    for shape in ((21, 21, 36), tuple(int(s) for s in args.pc_shape.split(','))):
+        net = PoseCellNetwork(shape, device=d.dev)
+        net.inject(1, tuple(s // 2 for s in shape))
+        n = args.node_calls
+        od = synthetic.odometry(n + 32, seed=0)
+        for v in od[:32]:
+            net.update(v)
+            net.posecells
+        t0 = time.perf_counter()
+        for v in od[32:32 + n]:
+            net.update(v)
+        t1 = time.perf_counter()
+        for v in od[32:32 + n]:
+            net.update(v)
+            p = net.posecells
+        t2 = time.perf_counter()
+        r0 = time.perf_counter()
+        for _ in range(n):
+            p = net.posecells
+        r1 = time.perf_counter()
+        assert p.shape == shape
+        net.close()
+        out['x'.join(map(str, shape))] = {
+            'update_us': 1e6 * (t1 - t0) / n, 'update_plus_read_us': 1e6 * (t2 - t1) / n,
+            'read_us': 1e6 * (r1 - r0) / n, 'node_steps_per_s': n / (t2 - t1),
+            'read_bytes': 8 * shape[0] * shape[1] * shape[2]}
+    out['note'] = ('update() then `.posecells` (float64, C order, a fresh array per read) per '
+                   'step, one host round trip each, as ros_simulate.py:134-145 does')
+    return out
+
+
 def host_info():
     model = platform.processor() or ''
     try:
@@ -412,7 +452,10 @@ def host_info():
     except (AttributeError, OSError):
         pass
     return {'cpu_model': model, 'os_cpu_count': os.cpu_count(), 'affinity_cpus': aff,
-            'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
+            'omp_num_threads': os.environ.get('OMP_NUM_THREADS'),
+            'cores_policy': 'OpenMP threads = OMP_NUM_THREADS as the GPU pool sets it (16, the host '
+                            'CPU share of one GPU on this pool); os_cpu_count and the affinity mask '
+                            'show the whole machine, which this job does not own'}
 
 
 def cpu_baseline(args):
@@ -517,6 +560,7 @@ def main():
         lib100 = bench_templates(args, d, total=args.library_total, steps=args.library_steps,
                                  warmup=1, bps=2)
     pc = bench_posecells(args, d)
+    pc['node_step'] = bench_node_step(args, d)
     pcs, st = None, None
     if not args.no_pc_stress:
         pcs = bench_posecell_stress(args, d)

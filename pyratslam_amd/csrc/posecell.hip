@@ -1908,6 +1908,26 @@ struct OdoTables {
     std::vector<int32_t> ownRows;
 };
 
+// Batched run(): full chunks of PC_CHUNK steps are replayed from hipGraphs captured
+// once per handle (two instances, so the host stages chunk c+1 while chunk c runs).
+// A graph is [control records pinned -> HBM, PC_CHUNK x (excite, path), (float64:
+// argmax reduction), key export to pinned host memory]: its kernel boundaries cost
+// 1.6 us against 2.8-3.4 us for stream launches (tools/ubench_launch.hip).
+constexpr int PC_CHUNK = 32;
+struct PcChunk {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    unsigned char* dCtl = nullptr;        // PC_CHUNK control records (HBM)
+    unsigned char* hCtl = nullptr;        // pinned staging, copied by the graph's first node
+    unsigned long long* dRes = nullptr;   // PC_CHUNK x RES_SLOTS argmax slots
+    unsigned long long* hRes = nullptr;   // pinned, coherent: one key per step
+    unsigned long long* hResDev = nullptr;
+    void* dArgV = nullptr;                // float64 per-block argmax partials
+    unsigned* dArgI = nullptr;
+    hipEvent_t done = nullptr;            // recorded after each replay
+    int first = -1;                       // first step (of the current run) in flight, -1: none
+};
+
 struct rs_pc {
     int X = 0, Y = 0, TH = 0, prec = RS_PREC_F32, device = 0;
     size_t n = 0, esz = 4;
@@ -1955,6 +1975,10 @@ struct rs_pc {
     std::vector<int32_t> cOx, cOy, cRows;
     std::vector<double> cZf;
     bool dbgSkipExport = false;  // rs_pc_debug(RS_PC_DBG_SKIP_EXPORT): the next run leaves hRes unwritten
+    int graphs = -1;             // chunk graphs for run(): -1 not built yet, 0 off (RS_PC_GRAPH=0), 1 built
+    double* hRead = nullptr;     // rs_pc_read: pinned float64 volume the export kernel writes in place
+    double* hReadDev = nullptr;
+    PcChunk chunk[2];
 };
 
 namespace {
@@ -2023,10 +2047,10 @@ int pc_check_ctl(const rs_pc* h, int n, const int32_t* ox, const int32_t* oy,
 }
 
 int pc_pack_ctl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
-                const double* zf) {
+                const double* zf, unsigned char* dst = nullptr) {
     const int TH = h->TH;
     for (int s = 0; s < n; ++s) {
-        unsigned char* rec = h->hCtl + (size_t)s * h->ctlStride;
+        unsigned char* rec = (dst ? dst : h->hCtl) + (size_t)s * h->ctlStride;
         std::memcpy(rec, ox + (size_t)s * TH, sizeof(int32_t) * TH);
         std::memcpy(rec + ctl_off_oy(h), oy + (size_t)s * TH, sizeof(int32_t) * TH);
         std::memcpy(rec + ctl_off_f(h), fidx + (size_t)s * TH, sizeof(int32_t) * TH);
@@ -2055,8 +2079,8 @@ void make_ctl_inline(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy
 }
 
 // ... or as pointers into the device ring record of step s.
-PcCtlRing make_ctl_ring(const rs_pc* h, int s) {
-    const unsigned char* rec = h->dCtl + (size_t)s * h->ctlStride;
+PcCtlRing make_ctl_ring(const rs_pc* h, int s, const unsigned char* ring = nullptr) {
+    const unsigned char* rec = (ring ? ring : h->dCtl) + (size_t)s * h->ctlStride;
     return PcCtlRing{reinterpret_cast<const int*>(rec),
                      reinterpret_cast<const int*>(rec + ctl_off_oy(h)),
                      reinterpret_cast<const int*>(rec + ctl_off_f(h)),
@@ -2102,14 +2126,30 @@ int pc_launch_stream(rs_pc* h, const T* P, T* Q, unsigned long long* slot, T* bm
     return RS_OK;
 }
 
+// Where step s of a launch sequence leaves its results: its RES_SLOTS argmax
+// slots, and (float64) its per-block argmax partials.
+struct StepOut {
+    unsigned long long* slot;
+    void* bmax;
+    unsigned* bidx;
+};
+inline StepOut step_out(unsigned long long* res, void* argv, unsigned* argi, size_t esz, int nblocks, int s) {
+    return StepOut{res + (size_t)s * RES_SLOTS,
+                   argv ? static_cast<char*>(argv) + esz * (size_t)s * nblocks : nullptr,
+                   argi ? argi + (size_t)s * nblocks : nullptr};
+}
+inline StepOut step_out(const rs_pc* h, int s) {
+    return step_out(h->dRes, h->dArgV, h->dArgI, h->esz, h->nPathBlocks, s);
+}
+
 template <typename T, typename CTL>
-int pc_launch_step(rs_pc* h, int s, const CTL* ctl, int prof_base) {
+int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
     const T* P = static_cast<const T*>(h->dP);
     T* Q = static_cast<T*>(h->dQ);
     const SepKernel<T>& k = sep_of<T>(h);
-    unsigned long long* slot = h->dRes + (size_t)s * RES_SLOTS;
-    T* bmax = h->dArgV ? static_cast<T*>(h->dArgV) + (size_t)s * h->nPathBlocks : nullptr;
-    unsigned* bidx = h->dArgI ? h->dArgI + (size_t)s * h->nPathBlocks : nullptr;
+    unsigned long long* slot = so.slot;
+    T* bmax = static_cast<T*>(so.bmax);
+    unsigned* bidx = so.bidx;
     const T* filt = static_cast<const T*>(h->dFilt);
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->cols) {
@@ -2187,13 +2227,10 @@ void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out) {
     out[0] = (int32_t)(xy / (unsigned)h->Y);
 }
 
-int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
-                const double* zf, int32_t* out_xyz) {
-    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
-    RS_CHECK(n >= 0, RS_ERR_ARG, "negative step count");
+// n steps launched one by one on the handle's stream, then one export and a sync.
+int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                  const double* zf, int32_t* out_xyz) {
     if (n == 0) return RS_OK;
-    RS_HIP(hipSetDevice(h->device));
-    RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
     RS_TRY(pc_grow_steps(h, n));
     // Batches: the column form takes each step's control as kernel arguments too (its
     // path kernel then starts its window loads without a global round trip for the
@@ -2218,15 +2255,15 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
             PcCtlInline c;
             make_ctl_inline(h, s, ox, oy, fidx, zf, &c);
             if (h->prec == RS_PREC_F32)
-                RS_TRY((pc_launch_step<float, PcCtlInline>(h, s, &c, pb)));
+                RS_TRY((pc_launch_step<float, PcCtlInline>(h, step_out(h, s), &c, pb)));
             else
-                RS_TRY((pc_launch_step<double, PcCtlInline>(h, s, &c, pb)));
+                RS_TRY((pc_launch_step<double, PcCtlInline>(h, step_out(h, s), &c, pb)));
         } else {
             const PcCtlRing c = make_ctl_ring(h, s);
             if (h->prec == RS_PREC_F32)
-                RS_TRY((pc_launch_step<float, PcCtlRing>(h, s, &c, pb)));
+                RS_TRY((pc_launch_step<float, PcCtlRing>(h, step_out(h, s), &c, pb)));
             else
-                RS_TRY((pc_launch_step<double, PcCtlRing>(h, s, &c, pb)));
+                RS_TRY((pc_launch_step<double, PcCtlRing>(h, step_out(h, s), &c, pb)));
         }
     }
     if (h->prec == RS_PREC_F64) {
@@ -2263,6 +2300,130 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         for (int s = 0; s < n; ++s)
             decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
     return RS_OK;
+}
+
+void pc_chunk_free(PcChunk& c) {
+    if (c.exec) (void)hipGraphExecDestroy(c.exec);
+    if (c.graph) (void)hipGraphDestroy(c.graph);
+    for (void* p : {(void*)c.dCtl, (void*)c.dRes, c.dArgV, (void*)c.dArgI})
+        if (p) (void)hipFree(p);
+    if (c.hCtl) (void)hipHostFree(c.hCtl);
+    if (c.hRes) (void)hipHostFree(c.hRes);
+    if (c.done) (void)hipEventDestroy(c.done);
+    c = PcChunk{};
+}
+
+// Capture chunk graph `ci` on the handle's stream (nothing else is queued on it:
+// every rs_pc_* call that launches work synchronises before it returns, inject aside,
+// which the caller's run() has already ordered before this point by synchronising).
+template <typename T>
+int pc_chunk_build(rs_pc* h, PcChunk& c) {
+    const int K = PC_CHUNK;
+    RS_HIP(hipMalloc(&c.dCtl, h->ctlStride * K));
+    RS_HIP(hipHostMalloc(&c.hCtl, h->ctlStride * K, hipHostMallocDefault));
+    std::memset(c.hCtl, 0, h->ctlStride * K);
+    RS_HIP(hipMalloc(&c.dRes, sizeof(unsigned long long) * RES_SLOTS * K));
+    RS_HIP(hipMemset(c.dRes, 0, sizeof(unsigned long long) * RES_SLOTS * K));
+    RS_HIP(hipHostMalloc(&c.hRes, sizeof(unsigned long long) * K, hipHostMallocMapped | hipHostMallocCoherent));
+    for (int s = 0; s < K; ++s) c.hRes[s] = RES_NONE;
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.hResDev), c.hRes, 0));
+    if (h->prec == RS_PREC_F64) {
+        RS_HIP(hipMalloc(&c.dArgV, h->esz * (size_t)K * h->nPathBlocks));
+        RS_HIP(hipMalloc(&c.dArgI, sizeof(unsigned) * (size_t)K * h->nPathBlocks));
+    }
+    RS_HIP(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    int st = RS_OK;
+    hipError_t e = hipMemcpyAsync(c.dCtl, c.hCtl, h->ctlStride * K, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) st = RS_ERR_HIP;
+    for (int s = 0; s < K && st == RS_OK; ++s) {
+        const PcCtlRing ctl = make_ctl_ring(h, s, c.dCtl);
+        st = pc_launch_step<T, PcCtlRing>(h, step_out(c.dRes, c.dArgV, c.dArgI, h->esz, h->nPathBlocks, s),
+                                          &ctl, -1);
+    }
+    if (st == RS_OK && h->prec == RS_PREC_F64)
+        hipLaunchKernelGGL((pc_argmax_steps<double>), dim3(K), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(c.dArgV), c.dArgI, h->nPathBlocks, c.dRes);
+    if (st == RS_OK) hipLaunchKernelGGL(pc_res_export, dim3(K), dim3(64), 0, h->stream, c.dRes, K, c.hResDev);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+    if (st != RS_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return st;
+    }
+    RS_CHECK(ec == hipSuccess && g, RS_ERR_HIP, "chunk graph capture failed: %s", hipGetErrorString(ec));
+    c.graph = g;
+    RS_HIP(hipGraphInstantiate(&c.exec, g, nullptr, nullptr, 0));
+    return RS_OK;
+}
+
+// The results of a replayed chunk: wait for it, check that every step's key
+// reached the host, decode.
+int pc_chunk_harvest(rs_pc* h, PcChunk& c, int32_t* out_xyz) {
+    if (c.first < 0) return RS_OK;
+    RS_HIP(hipEventSynchronize(c.done));
+    for (int s = 0; s < PC_CHUNK; ++s) {
+        RS_CHECK(c.hRes[s] != RES_NONE, RS_ERR_HIP,
+                 "step %d: its argmax key did not reach the host result buffer after the chunk "
+                 "graph completed", c.first + s);
+        if (out_xyz) decode_xyz(h, c.hRes[s], out_xyz + 3 * ((size_t)c.first + s));
+    }
+    c.first = -1;
+    return RS_OK;
+}
+
+int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                const double* zf, int32_t* out_xyz) {
+    RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    RS_CHECK(n >= 0, RS_ERR_ARG, "negative step count");
+    if (n == 0) return RS_OK;
+    RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
+    if (h->graphs < 0) {
+        const char* e = std::getenv("RS_PC_GRAPH");
+        h->graphs = (e && std::strcmp(e, "0") == 0) ? 0 : -2;  // -2: build on the first full chunk
+    }
+    const int K = PC_CHUNK;
+    if (h->graphs == 0 || h->profiling || h->dbgSkipExport || n < K)
+        return pc_run_direct(h, n, ox, oy, fidx, zf, out_xyz);
+    if (h->graphs == -2) {
+        for (PcChunk& c : h->chunk) {
+            const int st = h->prec == RS_PREC_F32 ? pc_chunk_build<float>(h, c) : pc_chunk_build<double>(h, c);
+            if (st != RS_OK) {
+                for (PcChunk& d : h->chunk) pc_chunk_free(d);
+                return st;
+            }
+        }
+        h->graphs = 1;
+    }
+    const size_t th = h->TH;
+    int s0 = 0, ci = 0;
+    int st = RS_OK;
+    for (; s0 + K <= n; s0 += K, ci ^= 1) {
+        PcChunk& c = h->chunk[ci];
+        if ((st = pc_chunk_harvest(h, c, out_xyz)) != RS_OK) break;   // chunk s0 - 2K
+        pc_pack_ctl(h, K, ox + th * s0, oy + th * s0, fidx + th * s0, zf + (size_t)FL * s0, c.hCtl);
+        for (int s = 0; s < K; ++s) c.hRes[s] = RES_NONE;
+        hipError_t e = hipGraphLaunch(c.exec, h->stream);
+        if (e == hipSuccess) e = hipEventRecord(c.done, h->stream);
+        if (e != hipSuccess) {
+            rs::set_error("chunk graph launch failed: %s", hipGetErrorString(e));
+            st = RS_ERR_HIP;
+            break;
+        }
+        c.first = s0;
+    }
+    // the remainder directly (it synchronises the stream), then the last chunks
+    if (st == RS_OK && s0 < n)
+        st = pc_run_direct(h, n - s0, ox + th * s0, oy + th * s0, fidx + th * s0, zf + (size_t)FL * s0,
+                           out_xyz ? out_xyz + 3 * (size_t)s0 : nullptr);
+    for (PcChunk& c : h->chunk) {
+        const int st2 = pc_chunk_harvest(h, c, out_xyz);
+        if (st == RS_OK) st = st2;
+        c.first = -1;
+    }
+    return st;
 }
 
 // path_integration's control for one step (posecell_network.py:252-308) in the
@@ -2598,6 +2759,8 @@ int rs_pc_destroy(rs_pc* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (PcChunk& c : h->chunk) pc_chunk_free(c);
+    if (h->hRead) (void)hipHostFree(h->hRead);
     for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
@@ -2637,11 +2800,11 @@ int rs_pc_excite(rs_pc* h) {
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
     if (h->prec == RS_PREC_F32) {
-        RS_TRY((pc_launch_step<float, PcCtlRing>(h, 0, nullptr, -1)));
+        RS_TRY((pc_launch_step<float, PcCtlRing>(h, step_out(h, 0), nullptr, -1)));
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
     } else {
-        RS_TRY((pc_launch_step<double, PcCtlRing>(h, 0, nullptr, -1)));
+        RS_TRY((pc_launch_step<double, PcCtlRing>(h, step_out(h, 0), nullptr, -1)));
         hipLaunchKernelGGL((pc_scale_kernel<double>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
     }
@@ -2805,15 +2968,29 @@ int rs_pc_read(rs_pc* h, double* host) {
     rs::clear_error();
     RS_CHECK(h && host, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
+    // The export kernel writes the float64 C-order volume straight into pinned host
+    // memory (one launch, no copy engine), then the host copies it into the caller's
+    // array; RS_PC_READ=dma exports to HBM and copies with hipMemcpyAsync instead.
+    static const bool dma = [] {
+        const char* e = std::getenv("RS_PC_READ");
+        return e && std::strcmp(e, "dma") == 0;
+    }();
+    if (!dma && !h->hRead) {
+        RS_HIP(hipHostMalloc(&h->hRead, sizeof(double) * h->n, hipHostMallocMapped | hipHostMallocCoherent));
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hReadDev), h->hRead, 0));
+    }
+    double* dst = dma ? h->dTmp : h->hReadDev;
+    const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
     if (h->prec == RS_PREC_F32)
-        hipLaunchKernelGGL((pc_export_kernel<float>), dim3(256), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)h->cols);
+        hipLaunchKernelGGL((pc_export_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
     else
-        hipLaunchKernelGGL((pc_export_kernel<double>), dim3(256), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)h->cols);
+        hipLaunchKernelGGL((pc_export_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
     RS_HIP(hipGetLastError());
-    RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+    if (dma) RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    if (!dma) std::memcpy(host, h->hRead, sizeof(double) * h->n);
     return RS_OK;
 }
 
@@ -2891,6 +3068,12 @@ int rs_pc_debug(rs_pc* h, int op) {
         if (h->dArgI)
             RS_HIP(hipMemsetAsync(h->dArgI, 0xFF, sizeof(unsigned) * (size_t)h->resCap * h->nPathBlocks, h->stream));
         for (int s = 0; s < h->resCap; ++s) h->hRes[s] = ~0ull;
+        for (PcChunk& c : h->chunk) {  // the chunk graphs' own slots and partials
+            if (c.dRes) RS_HIP(hipMemsetAsync(c.dRes, 0xFF, sizeof(unsigned long long) * RES_SLOTS * PC_CHUNK, h->stream));
+            if (c.dArgV) RS_HIP(hipMemsetAsync(c.dArgV, 0xFF, h->esz * (size_t)PC_CHUNK * h->nPathBlocks, h->stream));
+            if (c.dArgI)
+                RS_HIP(hipMemsetAsync(c.dArgI, 0xFF, sizeof(unsigned) * (size_t)PC_CHUNK * h->nPathBlocks, h->stream));
+        }
         RS_HIP(hipStreamSynchronize(h->stream));
         return RS_OK;
     }
