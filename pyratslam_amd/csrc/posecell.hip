@@ -1148,7 +1148,6 @@ constexpr int CO_TX = 8, CO_TY = 8, CO_NW = 12;
 // 2 output columns per task, window rows scheduled 2 at a time
 constexpr int CO_FSPLIT = 2, CO_FCOLS = 2, CO_FROWS = 2;
 constexpr int CO_CH = 8;                        // layers per theta-pass task (scalar stream/rows helpers)
-constexpr int CO_TCL = 2;                       // column theta passes: output layers per task
 constexpr int CO_LDS = 150 * 1024;              // LDS budget of the excitation kernel
 // Window rows are loaded as 16-byte vectors of VEC = 16 / sizeof(T) cells from a
 // VEC-aligned start (Y % VEC == 0, so a vector never straddles the wrap): a row of
@@ -1239,98 +1238,6 @@ __device__ inline CoLayers<CHUNK> co_layers(int ch, int KC, int TH) {
     return c;
 }
 
-// LDS vector slot of vector j of window row `row` (NCP vectors per row).  The
-// excitation window is read a row per lane as 16-byte vectors: with the whole
-// theta extent in LDS its rows are padded by one vector (odd pitch); a theta
-// chunk (two blocks per CU, no room for padding) XOR-swizzles the slots so 16
-// lanes reading 16 consecutive rows hit 16 distinct bank groups.  The path
-// window is plain.
-enum CoSlot { CO_PLAIN, CO_PADDED, CO_SWIZZLED };
-template <int NCP, int LAYOUT>
-__device__ inline int co_slot(int row, int j) {
-    if constexpr (LAYOUT == CO_SWIZZLED) return row * NCP + (j ^ ((row / (16 / NCP)) % NCP));
-    else if constexpr (LAYOUT == CO_PADDED) return row * (NCP + 1) + j;
-    else return row * NCP + j;
-}
-
-// Window vectors of a block in row order (element e -> layer L, row r, vector j).
-// (A two-part order, the block's own cells first and its halo after they had
-// landed so that the halo would come from neighbours' fetches in the XCD's L2,
-// measured slower -- 3.3 -> 3.9 us excitation loads -- with unchanged fabric
-// bytes per kernel: the halo reads were not served by L2.)
-template <int HX, int NCP>
-struct CoPart {
-    static constexpr int PER_LAYER = HX * NCP;
-    __device__ static inline void at(int e, int& L, int& r, int& j) {
-        L = e / PER_LAYER;
-        const int h = e - L * PER_LAYER;
-        r = h / NCP;
-        j = h - r * NCP;
-    }
-};
-
-template <typename T, int NT, int HX, int NCP, bool SHIFTED, bool CHUNK, typename PT, int U0 = 0, typename V, int LPT>
-__device__ inline void co_issue(V (&w)[LPT], const T* __restrict__ src, int X, int Y, int TH,
-                                const CoLayers<CHUNK>& ly, int x0, int y0, const int* s_ox, const int* s_oy) {
-    constexpr int VEC = co_vec<T>();
-    const int n = ly.nl * PT::PER_LAYER, tid = threadIdx.x;
-    const size_t lstride = (size_t)X * Y;
-#pragma clang loop unroll(full)
-    for (int u = 0; u < LPT; ++u) {
-        int L, r, j;
-        PT::at(min(tid + (U0 + u) * NT, n - 1), L, r, j);
-        int gr = co_wrap(x0 - HALF + r, X), gc = co_wrap(y0 - HALF, Y);
-        if constexpr (SHIFTED) {
-            gr += s_ox[L];
-            gr -= gr >= X ? X : 0;
-            gc += s_oy[L];
-            gc -= gc >= Y ? Y : 0;
-        }
-        // first vector at gc rounded down to VEC; vector j wraps as a unit.  A
-        // shifted row needs its last vector only when it starts more than
-        // (NCP - 1) * VEC - HY cells into its first vector; otherwise that lane
-        // re-reads the row's first vector (same line, no extra bytes; straight-line)
-        int jj = j;
-        if constexpr (SHIFTED)
-            jj = (j < NCP - 1 || (gc & (VEC - 1)) > (NCP - 1) * VEC - (2 * HALF + CO_TY)) ? j : 0;
-        w[u] = *reinterpret_cast<const V*>(src + (size_t)ly.global(L, TH) * lstride + (size_t)gr * Y +
-                                           co_wrap((gc & ~(VEC - 1)) + jj * VEC, Y));
-    }
-}
-
-template <int NT, int HX, int NCP, int LAYOUT, typename PT, int U0, bool CHUNK, typename T, typename V, int LPT,
-          int... U>
-__device__ inline void co_store_seq(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly,
-                                    std::integer_sequence<int, U...>) {
-    const int n = ly.nl * PT::PER_LAYER, tid = threadIdx.x;
-    auto one = [&](auto uc) __attribute__((always_inline)) {
-        constexpr int u = decltype(uc)::value;
-        const int e = tid + (U0 + u) * NT;
-        int L, r, j;
-        PT::at(e < n ? e : n - 1, L, r, j);
-        if (e < n) reinterpret_cast<V*>(s_in)[co_slot<NCP, LAYOUT>(L * HX + r, j)] = w[u];
-    };
-    (one(std::integral_constant<int, U>{}), ...);
-}
-// (an index sequence, not a loop: constant indices into w even where the unroller
-// gives up, so w stays in registers)
-template <int NT, int HX, int NCP, int LAYOUT, typename PT, int U0 = 0, bool CHUNK, typename T, typename V, int LPT>
-__device__ inline void co_store(const V (&w)[LPT], T* __restrict__ s_in, const CoLayers<CHUNK>& ly) {
-    co_store_seq<NT, HX, NCP, LAYOUT, PT, U0>(w, s_in, ly, std::make_integer_sequence<int, LPT>{});
-}
-
-// The whole window of a block into LDS, every load in flight together.
-template <typename T, int NT, int HX, int NCP, int THM, bool SHIFTED, int LAYOUT, bool CHUNK>
-__device__ inline void co_load_window(const T* __restrict__ src, T* __restrict__ s_in, int X, int Y, int TH,
-                                      const CoLayers<CHUNK>& ly, int x0, int y0, const int* s_ox,
-                                      const int* s_oy) {
-    using V = typename CoVec<T>::type;
-    using P0 = CoPart<HX, NCP>;
-    V w[(THM * P0::PER_LAYER + NT - 1) / NT];
-    co_issue<T, NT, HX, NCP, SHIFTED, CHUNK, P0>(w, src, X, Y, TH, ly, x0, y0, s_ox, s_oy);
-    co_store<NT, HX, NCP, LAYOUT, P0>(w, s_in, ly);
-}
-
 // Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
 // (:339-340) and the normalisation partial sum (:343) for one column tile.
 template <typename T, int TX, int TY, int NW, int THM, bool CHUNK>
@@ -1342,8 +1249,8 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
     constexpr int VEC = co_vec<T>();
     static_assert(TY % VEC == 0, "row vectors");
-    __shared__ __attribute__((aligned(16))) T s_in[2 * THM * TX * TY];  // the x-pass outputs (e, i)
-    __shared__ __attribute__((aligned(16))) T s_ye[THM * HX * TY];  // [r][L][c]
+    __shared__ __attribute__((aligned(16))) T s_in[2 * TX * TY * ((THM + 12 + 3) / 4 * 4)];  // x-pass outputs (e, i)
+    __shared__ __attribute__((aligned(16))) T s_ye[THM * HX * TY];  // [r][c][L]
     __shared__ __attribute__((aligned(16))) T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
     using V = typename CoVec<T>::type;
@@ -1360,7 +1267,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // consecutive words of one cell's theta column (whole 128-byte lines, where the
     // layer-major rows of 14 cells used a third of each line they touched).  Every
     // row of the block is in flight at once; the window never visits LDS; the y-pass
-    // outputs go to LDS as [r][L][c].
+    // outputs go to LDS as [r][c][L].
     {
         constexpr int NR = (THM * HX + NT - 1) / NT;
         const int nrow = ly.nl * HX;
@@ -1377,7 +1284,6 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             const int t = tid + u * NT;
             if (t >= nrow) break;
             const int r = t / ly.nl, L = t - r * ly.nl;
-            V oe[TY / VEC], oi[TY / VEC];
 #pragma unroll
             for (int c = 0; c < TY; ++c) {
                 T e = 0, g = 0;
@@ -1386,30 +1292,33 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
                     e += k.ge[q] * w[u][c + q];
                     g += k.gi[q] * w[u][c + q];
                 }
-                oe[c / VEC][c % VEC] = e;
-                oi[c / VEC][c % VEC] = g;
-            }
-#pragma unroll
-            for (int c = 0; c < TY / VEC; ++c) {
-                reinterpret_cast<V*>(s_ye + (r * THM + L) * TY)[c] = oe[c];
-                reinterpret_cast<V*>(s_yi + (r * THM + L) * TY)[c] = oi[c];
+                s_ye[(r * TY + c) * THM + L] = e;   // [r][c][L]: consecutive lanes, consecutive words
+                s_yi[(r * TY + c) * THM + L] = g;
             }
         }
     }
     PC_STAMP(5, 1);
     co_lds_barrier();
     PC_STAMP(5, 2);
-    // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows
+    // x pass: task (L, c) -> a column of TX outputs from HX y-pass rows, written as
+    // [cell p][SPO + L] rows of pitch PP (16-byte aligned: the theta pass reads
+    // them as vectors; consecutive lanes take consecutive layers, so the writes are
+    // conflict-free).  The whole-extent form also writes each output's wrapped copy
+    // (layers TH-4..TH-1 before SPO, 0..7 after SPO + TH), so every theta window is
+    // one contiguous aligned run with no extra pass.
+    constexpr int SPO = 4, PP = (THM + 12 + 3) / 4 * 4;
     T* s_xe = s_in;
-    T* s_xi = s_in + THM * TX * TY;
+    T* s_xi = s_in + TX * TY * PP;
     for (int t = tid; t < ly.nl * TY; t += NT) {
-        const int L = t / TY, c = t - L * TY;
+        const int c = t / ly.nl, L = t - c * ly.nl;
         T ye[HX], yi[HX];
 #pragma unroll
         for (int a = 0; a < HX; ++a) {
-            ye[a] = s_ye[(a * THM + L) * TY + c];
-            yi[a] = s_yi[(a * THM + L) * TY + c];
+            ye[a] = s_ye[(a * TY + c) * THM + L];
+            yi[a] = s_yi[(a * TY + c) * THM + L];
         }
+        // wrapped copies (TH >= 10, so at most one of each)
+        const int Lw1 = !CHUNK && L < 8 ? ly.nl + L : INT_MIN, Lw2 = !CHUNK && L >= ly.nl - 4 ? L - ly.nl : INT_MIN;
 #pragma unroll
         for (int i = 0; i < TX; ++i) {
             T e = 0, g = 0;
@@ -1418,50 +1327,75 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
                 e += k.ge[q] * ye[i + q];
                 g += k.gi[q] * yi[i + q];
             }
-            s_xe[(L * TX + i) * TY + c] = e;
-            s_xi[(L * TX + i) * TY + c] = g;
+            const int r = (i * TY + c) * PP + SPO;
+            s_xe[r + L] = e;
+            s_xi[r + L] = g;
+            if (Lw1 != INT_MIN) {
+                s_xe[r + Lw1] = e;
+                s_xi[r + Lw1] = g;
+            }
+            if (Lw2 != INT_MIN) {
+                s_xe[r + Lw2] = e;
+                s_xi[r + Lw2] = g;
+            }
         }
     }
     co_lds_barrier();
     PC_STAMP(5, 3);
-    // theta pass: task (row i, column vector cv, chunk j) -> CO_TCL output layers of
-    // VEC cells from CO_TCL + 6 x-pass layers read as 16-byte vectors; each output
-    // layer leaves as one 16-byte store
+    // theta pass: task (cell p, group j of VEC layers), consecutive lanes on
+    // consecutive groups of one cell: the outputs of a group are one 16-byte
+    // write-through store into Q, which is theta-fastest like P (the path kernel
+    // then loads whole runs of each cell's layers)
     double sum = 0.0;
     {
-        constexpr int CL = CO_TCL, NCV = TY / VEC;
-        const int ncl = (ly.nout + CL - 1) / CL;
+        const int ng = (ly.nout + VEC - 1) / VEC;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
-        for (int t = tid; t < TX * NCV * ncl; t += NT) {
-            const int j = t / (TX * NCV), rem = t - j * (TX * NCV), i = rem / NCV, cv = rem - i * NCV;
-            const int gi = x0 + i, gy = y0 + cv * VEC;
-            V xe[CL + 2 * HALF], xi[CL + 2 * HALF];
+        constexpr int ROFF = CHUNK ? 0 : 1, NRV = (ROFF + VEC + 2 * HALF + VEC - 1) / VEC;
+#pragma unroll 1
+        for (int t = tid; t < TX * TY * ng; t += NT) {
+            const int p = t / ng, j = t - p * ng, i = p / TY;
+            const int gi = x0 + i, gy = y0 + p - i * TY;
+            // taps of output lo = j * VEC + o: local layers lo - 3 .. lo + 3 (whole
+            // extent, from the aligned run starting at lo - 4) or lo .. lo + 6 (a chunk's
+            // local layer lo + 3 is its output lo)
+            const V* se = reinterpret_cast<const V*>(s_xe + p * PP + SPO + j * VEC - (CHUNK ? 0 : 4));
+            const V* si = reinterpret_cast<const V*>(s_xi + p * PP + SPO + j * VEC - (CHUNK ? 0 : 4));
+            T re[NRV * VEC], ri[NRV * VEC];
 #pragma unroll
-            for (int a = 0; a < CL + 2 * HALF; ++a) {
-                const int L = ly.tapc(j, a, CL, TH);
-                xe[a] = *reinterpret_cast<const V*>(s_xe + (L * TX + i) * TY + cv * VEC);
-                xi[a] = *reinterpret_cast<const V*>(s_xi + (L * TX + i) * TY + cv * VEC);
+            for (int q = 0; q < NRV; ++q) {
+                const V a = se[q], b = si[q];
+#pragma unroll
+                for (int c = 0; c < VEC; ++c) {
+                    re[q * VEC + c] = a[c];
+                    ri[q * VEC + c] = b[c];
+                }
             }
-            const bool mine = gi < X && gy < Y;
+            V qv;
 #pragma unroll
-            for (int o = 0; o < CL; ++o) {
-                const int lo = j * CL + o, gk = ly.k0 + lo;
-                V e = 0, g = 0;
+            for (int o = 0; o < VEC; ++o) {
+                T e = 0, g = 0;
 #pragma unroll
-                for (int q = 0; q < FL; ++q) {
-                    e += k.ge[q] * xe[o + q];
-                    g += k.gi[q] * xi[o + q];
+                for (int z = 0; z < FL; ++z) {
+                    e += k.ge[z] * re[ROFF + o + z];
+                    g += k.gi[z] * ri[ROFF + o + z];
                 }
-                const V v = (e - g) * k.scale;
-                V qv;
+                const T v = (e - g) * k.scale;
+                qv[o] = (v < k.inhib) ? T(0) : v - k.inhib;
+            }
+            if (gi < X && gy < Y) {
+                const int gk0 = ly.k0 + j * VEC, nv = min(VEC, ly.nout - j * VEC);
+                const size_t e0 = ((size_t)gi * Y + gy) * TH + gk0;
+                if (nv == VEC && e0 % VEC == 0) {
+                    co_put(Q, e0, qv, wt, nbytes);
+                } else {  // a ragged or unaligned group (TH or the chunk not a multiple of VEC)
 #pragma unroll
-                for (int c = 0; c < VEC; ++c) qv[c] = (v[c] < k.inhib) ? T(0) : v[c] - k.inhib;
-                if (mine && lo < ly.nout) {
-                    co_put(Q, ((size_t)gk * X + gi) * Y + gy, qv, wt, nbytes);
-#pragma unroll
-                    for (int c = 0; c < VEC; ++c) sum += (double)qv[c];
+                    for (int o = 0; o < VEC; ++o)
+                        if (o < nv) Q[e0 + o] = qv[o];
                 }
+#pragma unroll
+                for (int o = 0; o < VEC; ++o)
+                    if (o < nv) sum += (double)qv[o];
             }
         }
     }
@@ -1481,14 +1415,42 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
 // shifted 7x7 filter (:273 -> convolution.py:320-340), clamp (:300), 7-tap theta
 // filter (:310 -> convolution.py:344-359), clamp (:314), normalisation by the
 // excitation total (:343-345, applied at the end), fused argmax (:317-319).
+// Window buffer of the path kernel (bytes): the whole-extent form runs one block per
+// CU, the theta-chunked form two.
+constexpr int CO_WIN_BYTES = 128 * 1024, CO_WIN_BYTES_CHUNK = 56 * 1024;
+
+// signed shift in (-n/2, n/2] (control shifts may exceed the grid: vtrans large)
+__device__ inline int co_centre(int o, int n) {
+    o = rs::wrapi(o, n);
+    return o > n / 2 ? o - n : o;
+}
+
+__device__ inline int co_wave_min_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+    return v;
+}
+__device__ inline int co_wave_max_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
 template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL>
 __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
     const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
     T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx, int gy, int KC) {
-    constexpr int NT = 64 * NW, HX = TX + 2 * HALF;
-    constexpr int VEC = co_vec<T>(), NCP = co_ncp<T, true>(), RP = NCP * VEC, WN = HX * RP;
-    __shared__ __attribute__((aligned(16))) T s_in[THM * WN];  // [L][r][RP] shifted windows
+    constexpr int NT = 64 * NW, VEC = co_vec<T>();
+    // Q is theta-fastest, like P: the block loads the union of its layers' shifted
+    // windows -- WX x WY cells, each cell's run of layers contiguous in Q -- into LDS
+    // as [cell][layer] (pitch LP), in one pass when it fits (every |shift| <= 3 at
+    // 128x128x72: 20 x 20 cells x 72 layers, 115 KiB), else in passes of LC layers.
+    // Consecutive lanes take consecutive layers: the loads read whole runs of a
+    // cell's layers and the filter's LDS reads are conflict-free.  Shifts whose union
+    // window does not fit 8 layers per pass take per-layer windows instead.
+    constexpr int WBUF = (CHUNK ? CO_WIN_BYTES_CHUNK : CO_WIN_BYTES) / (int)sizeof(T);
+    __shared__ __attribute__((aligned(16))) T s_w[WBUF];
     // clamped 7x7 outputs [cell p][SPO + L], pitch PP (16-byte rows: the theta pass
     // reads VEC-aligned vectors); the whole-extent form also keeps wrapped copies of
     // the last 4 layers before SPO and of the first 8 after SPO + TH, so every theta
@@ -1496,7 +1458,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     constexpr int SPO = 4, PP = (THM + 12 + 3) / 4 * 4;
     __shared__ __attribute__((aligned(16))) T s_p[TX * TY * PP];
     __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
-    __shared__ int s_ox[THM], s_oy[THM], s_fo[THM], s_yd[THM];
+    __shared__ int s_ox[THM], s_oy[THM], s_fo[THM];
     __shared__ T s_bv[NW];
     __shared__ unsigned s_bl[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1504,13 +1466,10 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     PC_STAMP(6, 0);
-    // the normalisation partials' loads first (vmcnt waits are in issue order, so
-    // the reduction after the window loads are issued waits for these alone).
-    // Every wave forms the total itself: no block barrier between the window
-    // loads' issue and their use.
     // The control first (its loads are the ones the first barrier waits for; clamped
-    // unconditional reads, in flight together), then the partials (a guarded load
-    // had its wait hoisted to the kernel's start).
+    // unconditional reads, in flight together), then the normalisation partials (a
+    // guarded load had its wait hoisted to the kernel's start).  Every wave forms
+    // the total itself: no block barrier between the window loads and their use.
     static_assert(THM <= NT, "one layer's control per thread");
     const int Lc = min(tid, ly.nl - 1), gLc = ly.global(Lc, TH);
     const int oxc = ctl_ox(ctl, gLc), oyc = ctl_oy(ctl, gLc), fic = ctl_fi(ctl, gLc);
@@ -1519,15 +1478,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
     for (int u = 0; u < NPL; ++u) pt[u] = part[min(lane + 64 * u, npart - 1)];
     if (tid < ly.nl) {
-        s_ox[tid] = rs::wrapi(oxc, X);  // shifts may exceed the grid (vtrans large)
-        const int oy = rs::wrapi(oyc, Y);
-        s_oy[tid] = oy;
+        s_ox[tid] = co_centre(oxc, X);
+        s_oy[tid] = co_centre(oyc, Y);
         s_fo[tid] = fic * ST_FTP;
-        // window row (L, r) starts this many cells into its first vector
-        s_yd[tid] = co_wrap(co_wrap(y0 - HALF, Y) + oy, Y) & (co_vec<T>() - 1);
     }
     // the filter table's loads are issued now and land in LDS behind the window's
-    // (the first barrier waits for the shifts alone)
     constexpr int NFR = (RT_NFMAX * FT + NT - 1) / NT;
     T fr[NFR];
 #pragma unroll
@@ -1537,35 +1492,75 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
     co_lds_barrier();
     PC_STAMP(6, 1);
-    // window (L, r, c) <-> Q[L][(x0-3+r+ox[L]) % X][(y0-3+c+oy[L]) % Y], at LDS column
-    // c + d[L] of row (L, r), d[L] = (y0 - 3 + oy[L]) % Y % VEC
-    using P0 = CoPart<HX, NCP>;
-    constexpr int LPT = (THM * P0::PER_LAYER + NT - 1) / NT;
-    typename CoVec<T>::type win[LPT];
-    co_issue<T, NT, HX, NCP, true, CHUNK, P0>(win, Q, X, Y, TH, ly, x0, y0, s_ox, s_oy);
+    // the union window of the block's layers (every wave reduces the shifts itself)
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
+    for (int L = lane; L < ly.nl; L += 64) {
+        mnx = min(mnx, s_ox[L]);
+        mxx = max(mxx, s_ox[L]);
+        mny = min(mny, s_oy[L]);
+        mxy = max(mxy, s_oy[L]);
+    }
+    mnx = co_wave_min_i(mnx);
+    mxx = co_wave_max_i(mxx);
+    mny = co_wave_min_i(mny);
+    mxy = co_wave_max_i(mxy);
+    int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
+    const bool uni = WX <= X && WY <= Y && WX * WY * min(ly.nl, 8) <= WBUF;
+    if (!uni) {
+        WX = TX + 2 * HALF;
+        WY = TY + 2 * HALF;
+    }
+    const int ncell = WX * WY;
+    // layers per pass and their pitch (odd when it fits: fewer bank conflicts between
+    // lanes whose layers have different shifts)
+    const int LC = min(ly.nl, WBUF / ncell);
+    const int LP = (LC | 1) * ncell <= WBUF ? (LC | 1) : LC;
+    // window origin: the union's corner, or (per-layer mode) the layer's own
+    const int ux0 = co_wrap(x0 - HALF + mnx, X), uy0 = co_wrap(y0 - HALF + mny, Y);
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
     for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
     tot = co_wave_sum(tot);
     const T tt = (T)tot;
-    co_store<NT, HX, NCP, CO_PLAIN, P0>(win, s_in, ly);
 #pragma unroll
     for (int u = 0; u < NFR; ++u) {
         const int i = tid + u * NT, fi = i / FT;
         if (i < nf * FT) s_ftab[fi * ST_FTP + (i - fi * FT)] = fr[u];
     }
-    co_lds_barrier();
-    PC_STAMP(6, 2);
-    // 7x7 filter: task (L, column group, row part) -> TX/FS rows x CP columns of
-    // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each
-    // window row's reads; reads of CO_FROWS rows at a time in flight: hoisting all
-    // of them spills at 3 waves per SIMD)
     constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    {
-        for (int t = tid; t < ly.nl * NCG * FS; t += NT) {
-            const int L = t / (FS * NCG), rem = t - L * FS * NCG, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
+    constexpr int NLD = (WBUF + NT - 1) / NT;  // window loads per thread and pass (at most)
+    for (int Lb = 0; Lb < ly.nl; Lb += LC) {
+        const int lc = min(LC, ly.nl - Lb), nel = ncell * lc;
+        // window element e = (cell c, layer Lb + l), layer fastest
+        {
+            T w[NLD];
+#pragma unroll
+            for (int u = 0; u < NLD; ++u) {
+                const int e = min(tid + u * NT, nel - 1), c = e / lc, l = e - c * lc, L = Lb + l;
+                const int cu = c / WY, cv = c - cu * WY;
+                const int bx = uni ? ux0 : x0 - HALF + s_ox[L], by = uni ? uy0 : y0 - HALF + s_oy[L];
+                const int gr = co_wrap(co_wrap(bx, X) + cu, X), gc = co_wrap(co_wrap(by, Y) + cv, Y);
+                w[u] = Q[((size_t)gr * Y + gc) * TH + ly.global(L, TH)];
+            }
+#pragma unroll
+            for (int u = 0; u < NLD; ++u) {
+                const int e = tid + u * NT;
+                if (e < nel) {
+                    const int c = e / lc;
+                    s_w[c * LP + (e - c * lc)] = w[u];
+                }
+            }
+        }
+        co_lds_barrier();
+        if (Lb == 0) PC_STAMP(6, 2);
+        // 7x7 filter: task (layer, column group, row part) -> TX/FS rows x CP columns
+        // of outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each
+        // window row's reads; reads of CO_FROWS rows at a time in flight: hoisting all
+        // of them spills at 3 waves per SIMD).  Layer fastest over the lanes.
+        for (int t = tid; t < lc * NCG * FS; t += NT) {
+            const int l = t % lc, rem = t / lc, hf = rem / NCG, c0 = (rem - hf * NCG) * CP, L = Lb + l;
             T f[FT];
             st_filter<T>(s_ftab + s_fo[L], f);
             T acc[TXH][CP];
@@ -1573,12 +1568,13 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
             for (int i = 0; i < TXH; ++i)
 #pragma unroll
                 for (int c = 0; c < CP; ++c) acc[i][c] = 0;
-            const T* win = s_in + L * WN + hf * TXH * RP + s_yd[L] + c0;
+            const int dx = uni ? s_ox[L] - mnx : 0, dy = uni ? s_oy[L] - mny : 0;
+            const T* win = s_w + ((hf * TXH + dx) * WY + c0 + dy) * LP + l;
 #pragma unroll
             for (int a = 0; a < TXH + 2 * HALF; ++a) {
                 T w[FL + CP - 1];
 #pragma unroll
-                for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[a * RP + q];
+                for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WY + q) * LP];
                 if (a % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < TXH; ++i) {
@@ -1593,11 +1589,12 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
             for (int i = 0; i < TXH; ++i)
 #pragma unroll
-                for (int c = 0; c < CP; ++c) {
+                for (int c = 0; c < CP; ++c)
                     s_p[((hf * TXH + i) * TY + c0 + c) * PP + SPO + L] = acc[i][c] > T(0) ? acc[i][c] : T(0);
-                }
         }
+        if (Lb + LC < ly.nl) co_lds_barrier();  // the next pass overwrites the window
     }
+    (void)VEC;
     co_lds_barrier();
     if constexpr (!CHUNK) {  // the wrapped copies: layers TH-4..TH-1 before, 0..7 after
         for (int q = tid; q < TX * TY * 12; q += NT) {
@@ -1864,14 +1861,6 @@ __global__ void pc_import_kernel(const double* __restrict__ in, T* __restrict__ 
         P[thfast ? e : pc_layer_major(e, X, Y, TH)] = (T)in[e];
 }
 
-// layer-major Q -> theta-fastest P (the column form's rs_pc_excite: P = normalised Q)
-template <typename T>
-__global__ void pc_relayout_kernel(const T* __restrict__ Q, T* __restrict__ P, int X, int Y, int TH) {
-    const size_t n = (size_t)X * Y * TH;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
-         e += (size_t)gridDim.x * blockDim.x)
-        P[e] = Q[pc_layer_major(e, X, Y, TH)];
-}
 
 template <typename T>
 __global__ void pc_inject_kernel(T* __restrict__ P, size_t idx, double energy) {
@@ -1964,7 +1953,7 @@ struct rs_pc {
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
     bool cols = false;      // column kernels (RS_PC_FORM=cols[:KC]): TX x TY tiles through KC layers;
-                            // P is then theta-fastest (C order (x, y, th)), Q layer-major
+                            // P and Q are then theta-fastest (C order (x, y, th))
     int cgx = 0, cgy = 0;   // column tiles along x and y
     int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
@@ -2809,18 +2798,8 @@ int rs_pc_excite(rs_pc* h) {
                            static_cast<double*>(h->dQ), h->n, h->dPart, h->nPart);
     }
     RS_HIP(hipGetLastError());
-    if (h->cols) {  // P is theta-fastest on the column form, Q layer-major
-        if (h->prec == RS_PREC_F32)
-            hipLaunchKernelGGL((pc_relayout_kernel<float>), dim3(256), dim3(NT), 0, h->stream,
-                               static_cast<const float*>(h->dQ), static_cast<float*>(h->dP), h->X, h->Y, h->TH);
-        else
-            hipLaunchKernelGGL((pc_relayout_kernel<double>), dim3(256), dim3(NT), 0, h->stream,
-                               static_cast<const double*>(h->dQ), static_cast<double*>(h->dP), h->X, h->Y,
-                               h->TH);
-        RS_HIP(hipGetLastError());
-    } else {
-        RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
-    }
+    // Q has P's layout in every form (the column form: both theta-fastest)
+    RS_HIP(hipMemcpyAsync(h->dP, h->dQ, h->n * h->esz, hipMemcpyDeviceToDevice, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
 }

@@ -2,7 +2,8 @@
 """Static check of hand-counted vector-memory loads in a gfx9 device assembly
 listing (hipcc -S --cuda-device-only): for every kernel, walk its instructions
 in text order, keep the destination VGPRs of the vector-memory loads still in
-flight (vmcnt counts them in issue order) and report any instruction that reads
+flight (vmcnt counts them, and the stores and returnless atomics issued between
+them, in issue order) and report any instruction that reads
 or writes such a register before an `s_waitcnt vmcnt(N)` has retired the load.
 
 A hit is a real hazard on straight-line code: a read sees the register before
@@ -23,6 +24,9 @@ import sys
 
 LOAD = re.compile(r'^(global_load|buffer_load|flat_load|scratch_load)\w*\s+(\S+?),')
 WAIT = re.compile(r'^s_waitcnt\b(.*)')
+# vector-memory operations without a VGPR destination that still take a vmcnt slot
+VMEM_NODEST = re.compile(r'^(global_store|buffer_store|flat_store|scratch_store)\w*\s|'
+                         r'^(global_atomic|buffer_atomic|flat_atomic)\w*\s(?!.*\b(sc0|glc)\b)')
 REG = re.compile(r'\bv\[(\d+):(\d+)\]|\bv(\d+)\b')
 
 
@@ -98,6 +102,10 @@ def scan(name, body, asm_only):
                 hits.append((no, 'write', sorted(d & dest), lno, s))
         if m:
             inflight.append((dest, no, in_asm))
+        elif VMEM_NODEST.match(s):
+            # on gfx9 stores and returnless atomics count in vmcnt too: they hold a slot
+            # (no destination), so `vmcnt(N)` after them retires loads issued earlier
+            inflight.append((set(), no, in_asm))
     return hits
 
 
