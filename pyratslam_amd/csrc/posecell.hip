@@ -1144,6 +1144,10 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 // 12 waves per block (768 threads; 9, 10, 11, 13, 14, 16: 20.6, 20.3, 20.2, 20.5,
 // 20.3, 20.2 us vs 19.8 per 128x128x72 step)
 constexpr int CO_TX = 8, CO_TY = 8, CO_NW = 12;
+// float64 whole-extent blocks: 8 waves (2 per SIMD), so the path kernel's 7x7 filter
+// taps and its window loads fit the 256 VGPRs per wave without spilling
+template <typename T>
+__host__ __device__ constexpr int co_nw() { return sizeof(T) == 4 ? CO_NW : 8; }
 // 7x7 filter tasks of the path kernel: 2 tasks per output column (4-row halves),
 // 2 output columns per task, window rows scheduled 2 at a time
 constexpr int CO_FSPLIT = 2, CO_FCOLS = 2, CO_FROWS = 2;
@@ -1444,12 +1448,12 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     constexpr int NT = 64 * NW, VEC = co_vec<T>();
     // Q is theta-fastest, like P: the block loads the union of its layers' shifted
     // windows -- WX x WY cells, each cell's run of layers contiguous in Q -- into LDS
-    // as [cell][layer] (pitch LP), in one pass when it fits (every |shift| <= 3 at
-    // 128x128x72: 20 x 20 cells x 72 layers, 115 KiB), else in passes of LC layers.
-    // Consecutive lanes take consecutive layers: the loads read whole runs of a
-    // cell's layers and the filter's LDS reads are conflict-free.  Shifts whose union
-    // window does not fit 8 layers per pass take per-layer windows instead.
+    // as [cell][layer] (every |shift| <= 3 at 128x128x72: 20 x 20 cells x 72 layers,
+    // 115 KiB).  Consecutive lanes take consecutive layers: the loads read whole runs
+    // of a cell's layers and the filter's LDS reads are conflict-free.  Shifts whose
+    // union window does not fit take per-layer 14 x 14 windows instead.
     constexpr int WBUF = (CHUNK ? CO_WIN_BYTES_CHUNK : CO_WIN_BYTES) / (int)sizeof(T);
+    using V = typename CoVec<T>::type;
     __shared__ __attribute__((aligned(16))) T s_w[WBUF];
     // clamped 7x7 outputs [cell p][SPO + L], pitch PP (16-byte rows: the theta pass
     // reads VEC-aligned vectors); the whole-extent form also keeps wrapped copies of
@@ -1504,18 +1508,13 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     mxx = co_wave_max_i(mxx);
     mny = co_wave_min_i(mny);
     mxy = co_wave_max_i(mxy);
-    int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
-    const bool uni = WX <= X && WY <= Y && WX * WY * min(ly.nl, 8) <= WBUF;
-    if (!uni) {
-        WX = TX + 2 * HALF;
-        WY = TY + 2 * HALF;
-    }
-    const int ncell = WX * WY;
-    // layers per pass and their pitch (odd when it fits: fewer bank conflicts between
-    // lanes whose layers have different shifts)
-    const int LC = min(ly.nl, WBUF / ncell);
-    const int LP = (LC | 1) * ncell <= WBUF ? (LC | 1) : LC;
-    // window origin: the union's corner, or (per-layer mode) the layer's own
+    // window strides are compile-time (the filter's LDS reads take immediate offsets):
+    // WYP cells per window row, LPC layers per cell (odd: fewer bank conflicts between
+    // lanes whose layers have different shifts), at most WXP rows
+    constexpr int WYP = TY + 2 * HALF + 6, LPC = THM | 1, WXP = WBUF / (WYP * LPC);
+    static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
+    const int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
+    const bool uni = WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
     const int ux0 = co_wrap(x0 - HALF + mnx, X), uy0 = co_wrap(y0 - HALF + mny, Y);
     double tot = 0.0;
 #pragma unroll
@@ -1530,81 +1529,133 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     }
     constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    constexpr int NLD = (WBUF + NT - 1) / NT;  // window loads per thread and pass (at most)
-    for (int Lb = 0; Lb < ly.nl; Lb += LC) {
-        const int lc = min(LC, ly.nl - Lb), nel = ncell * lc;
-        // window element e = (cell c, layer Lb + l), layer fastest
-        {
-            T w[NLD];
+    const int nl = ly.nl;
+    if (uni && !CHUNK && TH % VEC == 0) {
+        // the common case: the union window (WX x WY cells) with 16-byte loads of VEC
+        // consecutive layers of a cell, positions advanced incrementally (no
+        // divisions per element); all of a thread's loads in flight together
+        constexpr int NV = (WXP * WYP * LPC / VEC + NT - 1) / NT;
+        // float64: two rounds of loads (all NV in flight spills the filter's registers)
+        constexpr int NR = sizeof(T) == 4 ? 1 : 2, NVR = (NV + NR - 1) / NR;
+        const int lcw = nl / VEC, nel = WX * WY * lcw;
+        const int c = tid / lcw, dc = NT / lcw, dl = (NT - dc * lcw) * VEC;
+        const int dcu = dc / WY, dcv = dc - dcu * WY;
+        int cu = c / WY, cv = c - cu * WY, l = (tid - c * lcw) * VEC;   // load cursor
+        int su = cu, sv = cv, sl = l;                                   // store cursor
+        auto advance = [&](int& u_, int& v_, int& l_) __attribute__((always_inline)) {
+            l_ += dl;
+            v_ += dcv;
+            u_ += dcu;
+            if (l_ >= nl) {
+                l_ -= nl;
+                ++v_;
+            }
+            if (v_ >= WY) {
+                v_ -= WY;
+                ++u_;
+            }
+        };
 #pragma unroll
-            for (int u = 0; u < NLD; ++u) {
-                const int e = min(tid + u * NT, nel - 1), c = e / lc, l = e - c * lc, L = Lb + l;
-                const int cu = c / WY, cv = c - cu * WY;
-                const int bx = uni ? ux0 : x0 - HALF + s_ox[L], by = uni ? uy0 : y0 - HALF + s_oy[L];
-                const int gr = co_wrap(co_wrap(bx, X) + cu, X), gc = co_wrap(co_wrap(by, Y) + cv, Y);
-                w[u] = Q[((size_t)gr * Y + gc) * TH + ly.global(L, TH)];
+        for (int r = 0; r < NR; ++r) {
+            V w[NVR];
+#pragma unroll
+            for (int k = 0; k < NVR; ++k) {
+                const int u = r * NVR + k;
+                if (u < NV && tid + u * NT < nel) {
+                    int gr = ux0 + cu, gc = uy0 + cv;
+                    gr -= gr >= X ? X : 0;
+                    gc -= gc >= Y ? Y : 0;
+                    w[k] = *reinterpret_cast<const V*>(Q + ((size_t)((unsigned)gr * Y + gc) * TH + l));
+                }
+                advance(cu, cv, l);
             }
 #pragma unroll
-            for (int u = 0; u < NLD; ++u) {
-                const int e = tid + u * NT;
+            for (int k = 0; k < NVR; ++k) {
+                const int u = r * NVR + k;
+                if (u < NV && tid + u * NT < nel) {
+                    T* d = s_w + (su * WYP + sv) * LPC + sl;
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) d[j] = w[k][j];
+                }
+                advance(su, sv, sl);
+            }
+        }
+    } else {
+        // theta chunks (a window run may wrap around TH), ragged extents, and shifts
+        // whose union window does not fit (each layer then takes its own 14 x 14
+        // window): scalar elements, 8 loads in flight per thread
+        const int wx = uni ? WX : TX + 2 * HALF, wy = uni ? WY : TY + 2 * HALF, nel = wx * wy * nl;
+        for (int e0 = tid; e0 < nel; e0 += 8 * NT) {
+            T w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * NT;
                 if (e < nel) {
-                    const int c = e / lc;
-                    s_w[c * LP + (e - c * lc)] = w[u];
+                    const int c = e / nl, L = e - c * nl, cu = c / wy, cv = c - cu * wy;
+                    const int bx = uni ? ux0 : co_wrap(x0 - HALF + s_ox[L], X);
+                    const int by = uni ? uy0 : co_wrap(y0 - HALF + s_oy[L], Y);
+                    w[u] = Q[((size_t)co_wrap(bx + cu, X) * Y + co_wrap(by + cv, Y)) * TH + ly.global(L, TH)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + u * NT;
+                if (e < nel) {
+                    const int c = e / nl, L = e - c * nl, cu = c / wy, cv = c - cu * wy;
+                    s_w[(cu * WYP + cv) * LPC + L] = w[u];
                 }
             }
         }
-        co_lds_barrier();
-        if (Lb == 0) PC_STAMP(6, 2);
-        // 7x7 filter: task (layer, column group, row part) -> TX/FS rows x CP columns
-        // of outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each
-        // window row's reads; reads of CO_FROWS rows at a time in flight: hoisting all
-        // of them spills at 3 waves per SIMD).  Layer fastest over the lanes.
-        for (int t = tid; t < lc * NCG * FS; t += NT) {
-            const int l = t % lc, rem = t / lc, hf = rem / NCG, c0 = (rem - hf * NCG) * CP, L = Lb + l;
-            T f[FT];
-            st_filter<T>(s_ftab + s_fo[L], f);
-            T acc[TXH][CP];
+    }
+    co_lds_barrier();
+    PC_STAMP(6, 2);
+    // 7x7 filter: task (layer, column group, row part) -> TX/FS rows x CP columns of
+    // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each window
+    // row's reads; reads of CO_FROWS rows at a time in flight: hoisting all of them
+    // spills at 3 waves per SIMD).  Layer fastest over the lanes.
+    for (int t = tid; t < nl * NCG * FS; t += NT) {
+        const int L = t % nl, rem = t / nl, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
+        T f[FT];
+        st_filter<T>(s_ftab + s_fo[L], f);
+        T acc[TXH][CP];
 #pragma unroll
-            for (int i = 0; i < TXH; ++i)
+        for (int i = 0; i < TXH; ++i)
 #pragma unroll
-                for (int c = 0; c < CP; ++c) acc[i][c] = 0;
-            const int dx = uni ? s_ox[L] - mnx : 0, dy = uni ? s_oy[L] - mny : 0;
-            const T* win = s_w + ((hf * TXH + dx) * WY + c0 + dy) * LP + l;
+            for (int c = 0; c < CP; ++c) acc[i][c] = 0;
+        const int dx = uni ? s_ox[L] - mnx : 0, dy = uni ? s_oy[L] - mny : 0;
+        const T* win = s_w + ((hf * TXH + dx) * WYP + c0 + dy) * LPC + L;
 #pragma unroll
-            for (int a = 0; a < TXH + 2 * HALF; ++a) {
-                T w[FL + CP - 1];
+        for (int a = 0; a < TXH + 2 * HALF; ++a) {
+            T w[FL + CP - 1];
 #pragma unroll
-                for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WY + q) * LP];
-                if (a % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
+            for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WYP + q) * LPC];
+            if (a % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int i = 0; i < TXH; ++i) {
-                    const int x = a - i;
-                    if (x < 0 || x >= FL) continue;
-#pragma unroll
-                    for (int c = 0; c < CP; ++c)
-#pragma unroll
-                        for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < TXH; ++i)
+            for (int i = 0; i < TXH; ++i) {
+                const int x = a - i;
+                if (x < 0 || x >= FL) continue;
 #pragma unroll
                 for (int c = 0; c < CP; ++c)
-                    s_p[((hf * TXH + i) * TY + c0 + c) * PP + SPO + L] = acc[i][c] > T(0) ? acc[i][c] : T(0);
+#pragma unroll
+                    for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
+            }
         }
-        if (Lb + LC < ly.nl) co_lds_barrier();  // the next pass overwrites the window
+        // with the wrapped copies of the whole-extent form (layers TH-4..TH-1 also
+        // before SPO, 0..7 also after SPO + TH; TH >= 10, so at most one of each)
+        const int Lw1 = !CHUNK && L < 8 ? nl + L : INT_MIN, Lw2 = !CHUNK && L >= nl - 4 ? L - nl : INT_MIN;
+#pragma unroll
+        for (int i = 0; i < TXH; ++i)
+#pragma unroll
+            for (int c = 0; c < CP; ++c) {
+                const T v = acc[i][c] > T(0) ? acc[i][c] : T(0);
+                T* sp = s_p + ((hf * TXH + i) * TY + c0 + c) * PP + SPO;
+                sp[L] = v;
+                if (Lw1 != INT_MIN) sp[Lw1] = v;
+                if (Lw2 != INT_MIN) sp[Lw2] = v;
+            }
     }
     (void)VEC;
     co_lds_barrier();
-    if constexpr (!CHUNK) {  // the wrapped copies: layers TH-4..TH-1 before, 0..7 after
-        for (int q = tid; q < TX * TY * 12; q += NT) {
-            const int p = q / 12, m = q - p * 12;
-            T* sp = s_p + p * PP + SPO;
-            if (m < 4) sp[m - 4] = sp[ly.nl - 4 + m];
-            else sp[ly.nl + m - 4] = sp[co_wrap(m - 4, ly.nl)];
-        }
-        co_lds_barrier();
-    }
     PC_STAMP(6, 3);
     // theta pass, clamp, normalisation, argmax: task (cell p, chunk j).  float32:
     // the first maximum as the largest packed (value, ~index) key; float64: value
@@ -1897,26 +1948,6 @@ struct OdoTables {
     std::vector<int32_t> ownRows;
 };
 
-// Batched run(): full chunks of PC_CHUNK steps are replayed from hipGraphs captured
-// once per handle (two instances, so the host stages chunk c+1 while chunk c runs).
-// A graph is [control records pinned -> HBM, PC_CHUNK x (excite, path), (float64:
-// argmax reduction), key export to pinned host memory]: its kernel boundaries cost
-// 1.6 us against 2.8-3.4 us for stream launches (tools/ubench_launch.hip).
-constexpr int PC_CHUNK = 32;
-struct PcChunk {
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
-    unsigned char* dCtl = nullptr;        // PC_CHUNK control records (HBM)
-    unsigned char* hCtl = nullptr;        // pinned staging, copied by the graph's first node
-    unsigned long long* dRes = nullptr;   // PC_CHUNK x RES_SLOTS argmax slots
-    unsigned long long* hRes = nullptr;   // pinned, coherent: one key per step
-    unsigned long long* hResDev = nullptr;
-    void* dArgV = nullptr;                // float64 per-block argmax partials
-    unsigned* dArgI = nullptr;
-    hipEvent_t done = nullptr;            // recorded after each replay
-    int first = -1;                       // first step (of the current run) in flight, -1: none
-};
-
 struct rs_pc {
     int X = 0, Y = 0, TH = 0, prec = RS_PREC_F32, device = 0;
     size_t n = 0, esz = 4;
@@ -1964,10 +1995,8 @@ struct rs_pc {
     std::vector<int32_t> cOx, cOy, cRows;
     std::vector<double> cZf;
     bool dbgSkipExport = false;  // rs_pc_debug(RS_PC_DBG_SKIP_EXPORT): the next run leaves hRes unwritten
-    int graphs = -1;             // chunk graphs for run(): -1 not built yet, 0 off (RS_PC_GRAPH=0), 1 built
     double* hRead = nullptr;     // rs_pc_read: pinned float64 volume the export kernel writes in place
     double* hReadDev = nullptr;
-    PcChunk chunk[2];
 };
 
 namespace {
@@ -2146,7 +2175,7 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
         const bool whole = h->coKC >= h->TH;
         constexpr int THF = co_thmax<T>(), THC = co_thmax_chunk<T>();
         if (whole)
-            hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW, THF, false>), g, dim3(64 * CO_NW), 0,
+            hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false>), g, dim3(64 * co_nw<T>()), 0,
                                h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH, h->cgx, h->cgy,
                                h->coKC, k);
         else
@@ -2158,7 +2187,7 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
         if (!ctl) return RS_OK;
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
         if (whole)
-            hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW, THF, false, CTL>), g, dim3(64 * CO_NW), 0,
+            hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false, CTL>), g, dim3(64 * co_nw<T>()), 0,
                                h->stream, Q, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf,
                                *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx, h->cgy, h->coKC);
         else
@@ -2291,77 +2320,6 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
     return RS_OK;
 }
 
-void pc_chunk_free(PcChunk& c) {
-    if (c.exec) (void)hipGraphExecDestroy(c.exec);
-    if (c.graph) (void)hipGraphDestroy(c.graph);
-    for (void* p : {(void*)c.dCtl, (void*)c.dRes, c.dArgV, (void*)c.dArgI})
-        if (p) (void)hipFree(p);
-    if (c.hCtl) (void)hipHostFree(c.hCtl);
-    if (c.hRes) (void)hipHostFree(c.hRes);
-    if (c.done) (void)hipEventDestroy(c.done);
-    c = PcChunk{};
-}
-
-// Capture chunk graph `ci` on the handle's stream (nothing else is queued on it:
-// every rs_pc_* call that launches work synchronises before it returns, inject aside,
-// which the caller's run() has already ordered before this point by synchronising).
-template <typename T>
-int pc_chunk_build(rs_pc* h, PcChunk& c) {
-    const int K = PC_CHUNK;
-    RS_HIP(hipMalloc(&c.dCtl, h->ctlStride * K));
-    RS_HIP(hipHostMalloc(&c.hCtl, h->ctlStride * K, hipHostMallocDefault));
-    std::memset(c.hCtl, 0, h->ctlStride * K);
-    RS_HIP(hipMalloc(&c.dRes, sizeof(unsigned long long) * RES_SLOTS * K));
-    RS_HIP(hipMemset(c.dRes, 0, sizeof(unsigned long long) * RES_SLOTS * K));
-    RS_HIP(hipHostMalloc(&c.hRes, sizeof(unsigned long long) * K, hipHostMallocMapped | hipHostMallocCoherent));
-    for (int s = 0; s < K; ++s) c.hRes[s] = RES_NONE;
-    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&c.hResDev), c.hRes, 0));
-    if (h->prec == RS_PREC_F64) {
-        RS_HIP(hipMalloc(&c.dArgV, h->esz * (size_t)K * h->nPathBlocks));
-        RS_HIP(hipMalloc(&c.dArgI, sizeof(unsigned) * (size_t)K * h->nPathBlocks));
-    }
-    RS_HIP(hipEventCreateWithFlags(&c.done, hipEventDisableTiming));
-    RS_HIP(hipStreamSynchronize(h->stream));
-    RS_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    int st = RS_OK;
-    hipError_t e = hipMemcpyAsync(c.dCtl, c.hCtl, h->ctlStride * K, hipMemcpyHostToDevice, h->stream);
-    if (e != hipSuccess) st = RS_ERR_HIP;
-    for (int s = 0; s < K && st == RS_OK; ++s) {
-        const PcCtlRing ctl = make_ctl_ring(h, s, c.dCtl);
-        st = pc_launch_step<T, PcCtlRing>(h, step_out(c.dRes, c.dArgV, c.dArgI, h->esz, h->nPathBlocks, s),
-                                          &ctl, -1);
-    }
-    if (st == RS_OK && h->prec == RS_PREC_F64)
-        hipLaunchKernelGGL((pc_argmax_steps<double>), dim3(K), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(c.dArgV), c.dArgI, h->nPathBlocks, c.dRes);
-    if (st == RS_OK) hipLaunchKernelGGL(pc_res_export, dim3(K), dim3(64), 0, h->stream, c.dRes, K, c.hResDev);
-    hipGraph_t g = nullptr;
-    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
-    if (st != RS_OK) {
-        if (g) (void)hipGraphDestroy(g);
-        return st;
-    }
-    RS_CHECK(ec == hipSuccess && g, RS_ERR_HIP, "chunk graph capture failed: %s", hipGetErrorString(ec));
-    c.graph = g;
-    RS_HIP(hipGraphInstantiate(&c.exec, g, nullptr, nullptr, 0));
-    return RS_OK;
-}
-
-// The results of a replayed chunk: wait for it, check that every step's key
-// reached the host, decode.
-int pc_chunk_harvest(rs_pc* h, PcChunk& c, int32_t* out_xyz) {
-    if (c.first < 0) return RS_OK;
-    RS_HIP(hipEventSynchronize(c.done));
-    for (int s = 0; s < PC_CHUNK; ++s) {
-        RS_CHECK(c.hRes[s] != RES_NONE, RS_ERR_HIP,
-                 "step %d: its argmax key did not reach the host result buffer after the chunk "
-                 "graph completed", c.first + s);
-        if (out_xyz) decode_xyz(h, c.hRes[s], out_xyz + 3 * ((size_t)c.first + s));
-    }
-    c.first = -1;
-    return RS_OK;
-}
-
 int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                 const double* zf, int32_t* out_xyz) {
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
@@ -2369,50 +2327,7 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (n == 0) return RS_OK;
     RS_HIP(hipSetDevice(h->device));
     RS_TRY(pc_check_ctl(h, n, ox, oy, fidx, zf));
-    if (h->graphs < 0) {
-        const char* e = std::getenv("RS_PC_GRAPH");
-        h->graphs = (e && std::strcmp(e, "0") == 0) ? 0 : -2;  // -2: build on the first full chunk
-    }
-    const int K = PC_CHUNK;
-    if (h->graphs == 0 || h->profiling || h->dbgSkipExport || n < K)
-        return pc_run_direct(h, n, ox, oy, fidx, zf, out_xyz);
-    if (h->graphs == -2) {
-        for (PcChunk& c : h->chunk) {
-            const int st = h->prec == RS_PREC_F32 ? pc_chunk_build<float>(h, c) : pc_chunk_build<double>(h, c);
-            if (st != RS_OK) {
-                for (PcChunk& d : h->chunk) pc_chunk_free(d);
-                return st;
-            }
-        }
-        h->graphs = 1;
-    }
-    const size_t th = h->TH;
-    int s0 = 0, ci = 0;
-    int st = RS_OK;
-    for (; s0 + K <= n; s0 += K, ci ^= 1) {
-        PcChunk& c = h->chunk[ci];
-        if ((st = pc_chunk_harvest(h, c, out_xyz)) != RS_OK) break;   // chunk s0 - 2K
-        pc_pack_ctl(h, K, ox + th * s0, oy + th * s0, fidx + th * s0, zf + (size_t)FL * s0, c.hCtl);
-        for (int s = 0; s < K; ++s) c.hRes[s] = RES_NONE;
-        hipError_t e = hipGraphLaunch(c.exec, h->stream);
-        if (e == hipSuccess) e = hipEventRecord(c.done, h->stream);
-        if (e != hipSuccess) {
-            rs::set_error("chunk graph launch failed: %s", hipGetErrorString(e));
-            st = RS_ERR_HIP;
-            break;
-        }
-        c.first = s0;
-    }
-    // the remainder directly (it synchronises the stream), then the last chunks
-    if (st == RS_OK && s0 < n)
-        st = pc_run_direct(h, n - s0, ox + th * s0, oy + th * s0, fidx + th * s0, zf + (size_t)FL * s0,
-                           out_xyz ? out_xyz + 3 * (size_t)s0 : nullptr);
-    for (PcChunk& c : h->chunk) {
-        const int st2 = pc_chunk_harvest(h, c, out_xyz);
-        if (st == RS_OK) st = st2;
-        c.first = -1;
-    }
-    return st;
+    return pc_run_direct(h, n, ox, oy, fidx, zf, out_xyz);
 }
 
 // path_integration's control for one step (posecell_network.py:252-308) in the
@@ -2748,7 +2663,6 @@ int rs_pc_destroy(rs_pc* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (PcChunk& c : h->chunk) pc_chunk_free(c);
     if (h->hRead) (void)hipHostFree(h->hRead);
     for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
@@ -3047,12 +2961,6 @@ int rs_pc_debug(rs_pc* h, int op) {
         if (h->dArgI)
             RS_HIP(hipMemsetAsync(h->dArgI, 0xFF, sizeof(unsigned) * (size_t)h->resCap * h->nPathBlocks, h->stream));
         for (int s = 0; s < h->resCap; ++s) h->hRes[s] = ~0ull;
-        for (PcChunk& c : h->chunk) {  // the chunk graphs' own slots and partials
-            if (c.dRes) RS_HIP(hipMemsetAsync(c.dRes, 0xFF, sizeof(unsigned long long) * RES_SLOTS * PC_CHUNK, h->stream));
-            if (c.dArgV) RS_HIP(hipMemsetAsync(c.dArgV, 0xFF, h->esz * (size_t)PC_CHUNK * h->nPathBlocks, h->stream));
-            if (c.dArgI)
-                RS_HIP(hipMemsetAsync(c.dArgI, 0xFF, sizeof(unsigned) * (size_t)PC_CHUNK * h->nPathBlocks, h->stream));
-        }
         RS_HIP(hipStreamSynchronize(h->stream));
         return RS_OK;
     }

@@ -8,7 +8,8 @@ or writes such a register before an `s_waitcnt vmcnt(N)` has retired the load.
 
 A hit is a real hazard on straight-line code: a read sees the register before
 the data lands, a write is clobbered when the data lands.  (The walk ignores
-branches, so a hit across a loop back edge is approximate.)
+conditional branches, so a hit across a loop back edge is approximate; after an
+unconditional jump only inline-asm loads stay tracked.)
 
 This is the evidence behind DESIGN.md's account of the round-1 illegal-address
 fault: the inline-asm window loads of the old stream kernels (commit f7be589^)
@@ -68,6 +69,12 @@ def scan(name, body, asm_only):
             in_asm = False
             continue
         if not s or s.startswith('.') or s.endswith(':'):
+            continue
+        if re.match(r'^(s_branch|s_setpc_b64|s_endpgm)\b', s):
+            # the text after an unconditional jump is not its fall-through: the
+            # compiler's own loads are waited for on the real path (hipcc places
+            # their waits on the CFG); keep tracking only the asm loads it cannot see
+            inflight = [x for x in inflight if x[2]]
             continue
         w = WAIT.match(s)
         if w:

@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
     std::vector<int32_t> ox(n * TH, 1), oy(n * TH, -1), f(n * TH, 0), out(3 * n);
     std::vector<double> zf(n * 7, 0.1);
     for (int s = 0; s < n; ++s) zf[s * 7 + 3] = 0.4;
+    fprintf(stderr, "created, form %s\n", rs_pc_step_form(h));
     for (int rep = 0; rep < 3; ++rep)
         if (rs_pc_run(h, n, ox.data(), oy.data(), f.data(), zf.data(), out.data()) != RS_OK) {
             fprintf(stderr, "run: %s\n", rs_last_error());
@@ -68,7 +69,9 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < reps; ++rep)
         if (rs_pc_run(h, n, ox.data(), oy.data(), f.data(), zf.data(), out.data()) != RS_OK) return 1;
     const double direct = (now_us() - t0) / (reps * n);
+    fprintf(stderr, "rs_pc_run timed\n");
     // the same n steps captured (ring control uploaded once, outside the graph)
+    if (pc_grow_steps(h, n) != RS_OK) return 1;
     pc_pack_ctl(h, n, ox.data(), oy.data(), f.data(), zf.data());
     CK(hipMemcpy(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice));
     hipGraph_t g;
@@ -80,6 +83,7 @@ int main(int argc, char** argv) {
     }
     hipLaunchKernelGGL(pc_res_export, dim3(n), dim3(64), 0, h->stream, h->dRes, n, h->hResDev);
     CK(hipStreamEndCapture(h->stream, &g));
+    fprintf(stderr, "captured\n");
     double ti = now_us();
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     const double inst = now_us() - ti;
@@ -100,7 +104,8 @@ int main(int argc, char** argv) {
     }
     CK(hipStreamSynchronize(h->stream));
     const double ring = (now_us() - t0) / (reps * n);
-    printf("grid %dx%dx%d form %s: rs_pc_run %.2f us/step; ring launches %.2f us/step; graph replay %.2f "
+    printf("grid %dx%dx%d form %s: rs_pc_run %.2f us/step; ring launches %.2f us/step; "
+           "one graph of all steps %.2f "
            "us/step (instantiate %.0f us for %d steps)\n",
            X, Y, TH, rs_pc_step_form(h), direct, ring, graph, inst, n);
     rs_pc_destroy(h);
