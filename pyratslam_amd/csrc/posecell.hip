@@ -1429,15 +1429,16 @@ __device__ inline int co_centre(int o, int n) {
     return o > n / 2 ? o - n : o;
 }
 
-__device__ inline int co_wave_min_i(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
-    return v;
-}
-__device__ inline int co_wave_max_i(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-    return v;
+// wave min / max of an int by DPP row operations and readlanes (as co_wave_max)
+template <bool MAX>
+__device__ inline int co_wave_ext_i(int v) {
+    auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));
+    return op(op(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+              op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
 template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL>
@@ -1486,7 +1487,6 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         s_oy[tid] = co_centre(oyc, Y);
         s_fo[tid] = fic * ST_FTP;
     }
-    // the filter table's loads are issued now and land in LDS behind the window's
     constexpr int NFR = (RT_NFMAX * FT + NT - 1) / NT;
     T fr[NFR];
 #pragma unroll
@@ -1494,28 +1494,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     T zf[FL];
 #pragma unroll
     for (int z = 0; z < FL; ++z) zf[z] = (T)ctl_zf(ctl, z);
-    co_lds_barrier();
-    PC_STAMP(6, 1);
-    // the union window of the block's layers (every wave reduces the shifts itself)
-    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
-    for (int L = lane; L < ly.nl; L += 64) {
-        mnx = min(mnx, s_ox[L]);
-        mxx = max(mxx, s_ox[L]);
-        mny = min(mny, s_oy[L]);
-        mxy = max(mxy, s_oy[L]);
-    }
-    mnx = co_wave_min_i(mnx);
-    mxx = co_wave_max_i(mxx);
-    mny = co_wave_min_i(mny);
-    mxy = co_wave_max_i(mxy);
-    // window strides are compile-time (the filter's LDS reads take immediate offsets):
-    // WYP cells per window row, LPC layers per cell (odd: fewer bank conflicts between
-    // lanes whose layers have different shifts), at most WXP rows
-    constexpr int WYP = TY + 2 * HALF + 6, LPC = THM | 1, WXP = WBUF / (WYP * LPC);
-    static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
-    const int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
-    const bool uni = WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
-    const int ux0 = co_wrap(x0 - HALF + mnx, X), uy0 = co_wrap(y0 - HALF + mny, Y);
+    // the normalisation total (every wave forms it itself) and the filter table into
+    // LDS before the first barrier, which waits for the control's loads anyway: the
+    // window's loads then follow with nothing else to wait for
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
@@ -1527,6 +1508,29 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         const int i = tid + u * NT, fi = i / FT;
         if (i < nf * FT) s_ftab[fi * ST_FTP + (i - fi * FT)] = fr[u];
     }
+    co_lds_barrier();
+    PC_STAMP(6, 1);
+    // the union window of the block's layers (every wave reduces the shifts itself)
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
+    for (int L = lane; L < ly.nl; L += 64) {
+        mnx = min(mnx, s_ox[L]);
+        mxx = max(mxx, s_ox[L]);
+        mny = min(mny, s_oy[L]);
+        mxy = max(mxy, s_oy[L]);
+    }
+    mnx = co_wave_ext_i<false>(mnx);
+    mxx = co_wave_ext_i<true>(mxx);
+    mny = co_wave_ext_i<false>(mny);
+    mxy = co_wave_ext_i<true>(mxy);
+    // window strides are compile-time (the filter's LDS reads take immediate offsets):
+    // WYP cells per window row, LPC layers per cell (odd: fewer bank conflicts between
+    // lanes whose layers have different shifts), at most WXP rows
+    constexpr int WYP = TY + 2 * HALF + 6, LPC = THM | 1, WXP = WBUF / (WYP * LPC);
+    static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
+    const int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
+    const bool uni = WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
+    const int ux0 = co_wrap(x0 - HALF + mnx, X), uy0 = co_wrap(y0 - HALF + mny, Y);
+
     constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
     const int nl = ly.nl;
@@ -1561,11 +1565,13 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
             for (int k = 0; k < NVR; ++k) {
                 const int u = r * NVR + k;
-                if (u < NV && tid + u * NT < nel) {
+                if (u < NV) {  // straight-line: a thread past the window re-reads element 0
                     int gr = ux0 + cu, gc = uy0 + cv;
                     gr -= gr >= X ? X : 0;
                     gc -= gc >= Y ? Y : 0;
-                    w[k] = *reinterpret_cast<const V*>(Q + ((size_t)((unsigned)gr * Y + gc) * TH + l));
+                    const unsigned off = tid + u * NT < nel ? ((unsigned)gr * Y + gc) * TH + l
+                                                            : ((unsigned)ux0 * Y + uy0) * TH;
+                    w[k] = *reinterpret_cast<const V*>(Q + off);
                 }
                 advance(cu, cv, l);
             }

@@ -43,7 +43,7 @@ static double median(std::vector<double> v) {
 
 int main(int argc, char** argv) {
     int X = 64, Y = 64, TH = 36;
-    if (argc == 4) {
+    if (argc >= 4) {
         X = atoi(argv[1]);
         Y = atoi(argv[2]);
         TH = atoi(argv[3]);
@@ -77,6 +77,17 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
     const int n = 200;
     std::vector<int32_t> ox(n * TH, 1), oy(n * TH, -1), f(n * TH, 0), out(3 * n);
+    // argv[4] = translation in cells: the per-layer shifts of that step, round(vt cos),
+    // round(vt sin) of each layer's heading (posecell_network.py:257-265), as run() sees
+    if (argc >= 5) {
+        const double vt = atof(argv[4]);
+        for (int s = 0; s < n; ++s)
+            for (int k = 0; k < TH; ++k) {
+                const double a = (k - TH / 2) * 2 * M_PI / TH;
+                ox[s * TH + k] = (int)std::nearbyint(vt * std::cos(a));
+                oy[s * TH + k] = (int)std::nearbyint(vt * std::sin(a));
+            }
+    }
     std::vector<double> zf(n * 7, 0.1);
     for (int s = 0; s < n; ++s) zf[s * 7 + 3] = 0.4;
     for (int rep = 0; rep < 3; ++rep)
