@@ -470,6 +470,26 @@ def cpu_baseline(args):
     qs, _ = synthetic.queries(lib, 4096, seed=2)
     budget = args.cpu_seconds
     host = host_info()
+    # thread count: OMP_NUM_THREADS as the pool sets it (its CPU share of one GPU)
+    # and the affinity mask's size (all host cores) are both tried on a
+    # short sample; the faster one runs the baseline (a mask wider than the job's
+    # CPU quota oversubscribes it)
+    cands = sorted({c for c in (C.threads(), host['affinity_cpus'] or 0) if c > 0})
+    probe = {}
+    for c in cands:
+        C.set_threads(c)
+        C.vt_best(lib, qs[:64])                      # thread pool up
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < min(1.0, budget / 4):
+            C.vt_best(lib, qs[n % 4096:n % 4096 + 64])
+            n += 64
+        probe[c] = n / (time.perf_counter() - t0)
+    best = max(probe, key=probe.get)
+    C.set_threads(best)
+    host = dict(host, thread_probe_queries_per_s={str(k): round(v, 1) for k, v in probe.items()},
+                cores_policy='OpenMP threads: the faster of OMP_NUM_THREADS and the affinity '
+                              'mask size on a short probe (thread_probe_queries_per_s)')
     # C / OpenMP: template compares
     n = 0
     t0 = time.perf_counter()

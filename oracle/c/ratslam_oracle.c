@@ -37,6 +37,16 @@ int ro_threads(void) {
 #endif
 }
 
+/* bench.py's cpu_baseline picks the thread count (OMP_NUM_THREADS or the affinity
+ * mask's size, whichever runs faster on the box) */
+void ro_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 void ro_conv3d(const double* P, const double* K, double* out, int X, int Y, int TH) {
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < X; ++i)

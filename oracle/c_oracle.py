@@ -22,6 +22,7 @@ def load(build=True):
         vp = ctypes.c_void_p
         i = ctypes.c_int
         _lib.ro_threads.restype = i
+        _lib.ro_set_threads.argtypes = [i]
         _lib.ro_update.argtypes = [vp, vp, vp, ctypes.c_double, vp, vp, vp, vp, i, i, i, vp]
         _lib.ro_vt_scores.argtypes = [vp, ctypes.c_int64, vp, i, i, i, vp]
         _lib.ro_vt_best.argtypes = [vp, ctypes.c_int64, vp, i, i, i, i, vp, vp]
@@ -75,3 +76,7 @@ def vt_best(library, queries, max_offset=8):
 
 def threads():
     return load().ro_threads()
+
+
+def set_threads(n):
+    load().ro_set_threads(int(n))
