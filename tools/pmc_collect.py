@@ -22,6 +22,7 @@ import glob
 import json
 import os
 import re
+import shutil
 
 SCANS = {'headline': (1000, 10240), 'stress': (10000, 5120), 'library': (100000, 2048)}
 PCS = {'pc64': ('rows', [64, 64, 36]), 'pc128': ('cols', [128, 128, 72])}
@@ -142,6 +143,29 @@ def main():
             continue
         summary['configs'][c] = summarise(a.dir, c)
     traffic = traffic_of(summary['configs'], a.tag)
+    # the raw inputs of every figure, tracked: each configuration's rocprofv3
+    # kernel_stats.csv and its per-kernel counter averages (one row per kernel and
+    # counter) under profiles/<tag>/, named in pmc_traffic.json's source fields
+    raw = os.path.join(a.out, a.tag)
+    os.makedirs(raw, exist_ok=True)
+    for c in summary['configs']:
+        f = find(os.path.join(a.dir, c + '_trace'), '*kernel_stats.csv')
+        if f:
+            shutil.copy(f, os.path.join(raw, f'{c}_kernel_stats.csv'))
+        with open(os.path.join(raw, f'{c}_counters.csv'), 'w', newline='') as fh:
+            wr = csv.writer(fh)
+            wr.writerow(['pass', 'kernel', 'counter', 'dispatches', 'mean_value'])
+            for ps in ('fetch', 'write', 'sq'):
+                for k, cs in sorted(counters(os.path.join(a.dir, f'{c}_{ps}')).items()):
+                    for n, v in sorted(cs.items()):
+                        wr.writerow([ps, k, n, len(v), repr(sum(v) / len(v))])
+    f = find(os.path.join(a.dir, 'bench_trace'), '*kernel_stats.csv')
+    if f:
+        shutil.copy(f, os.path.join(raw, 'bench_kernel_stats.csv'))
+    for c, rec in list(traffic['scans'].items()) + list(traffic['pose_cell'].items()):
+        cfg = c if c in SCANS else {'rows': 'pc64', 'cols': 'pc128'}[c]
+        rec['kernel_us_source'] = f'profiles/{a.tag}/{cfg}_kernel_stats.csv (AverageNs)'
+        rec['counter_source'] = f'profiles/{a.tag}/{cfg}_counters.csv'
     bench = trace_stats(os.path.join(a.dir, 'bench_trace'))
     if bench:
         summary['bench_command'] = {'command': 'python bench.py', 'kernels': bench}

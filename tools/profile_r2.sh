@@ -13,9 +13,9 @@ cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
 declare -A CMD=(
-  [headline]="scan --templates 1000 --queries 10240 --launches 20"
-  [stress]="scan --templates 10000 --queries 5120 --launches 6"
-  [library]="scan --templates 100000 --queries 2048 --launches 3"
+  [headline]="scan --templates 1000 --queries 10240 --launches 60"
+  [stress]="scan --templates 10000 --queries 5120 --launches 16"
+  [library]="scan --templates 100000 --queries 2048 --launches 6"
   [pc64]="pc --shape 64,64,36 --steps 400"
   [pc128]="pc --shape 128,128,72 --steps 300"
 )

@@ -38,21 +38,30 @@ def clock_warmup(ms, kind):
 
 
 def scan(a):
+    """The bench's own path: one rs_vt_match_stream call per launch over
+    queries / 1024 HBM-resident batches of 1,024 queries (one plane-scan launch of
+    all of them), calls back to back, so the profiled dispatches run as the bench's
+    timed ones do."""
     from pyratslam_amd import _lib, synthetic
     from pyratslam_amd.view_templates import ViewTemplates
     vts = ViewTemplates._from_shape((64, 32), 45000, capacity=a.templates)
     for lo in range(0, a.templates, 8192):
         vts.add(synthetic.library(min(8192, a.templates - lo), seed=1, first=lo))
     qlib = synthetic.library(min(a.templates, 4096), seed=1)
-    qs, src = synthetic.queries_fast(qlib, a.queries, seed=2)
+    bq = min(1024, a.queries)
+    nb = max(1, a.queries // bq)
+    qs, src = synthetic.queries_fast(qlib, nb * bq, seed=2)
+    buf = _lib.DeviceBuffer(qs.nbytes).upload(qs)
     clock_warmup(a.clock_warmup_ms, 'scan')
-    idx, _, _ = vts.match_templates(qs, mode=_lib.RS_VT_FROZEN)
-    ok = bool(np.all(idx[src >= 0] == src[src >= 0]))
+    sidx, _ = vts.match_stream((nb, bq, buf.offset(0)))
+    got = np.asarray(sidx).reshape(-1)
+    ok = bool(np.all(got[src >= 0] == src[src >= 0]))
+    vts.set_timing(True)
     ms = []
     for _ in range(a.launches):
-        vts.match_templates(qs, mode=_lib.RS_VT_FROZEN)
+        vts.match_stream((nb, bq, buf.offset(0)))
         ms.append(vts.device_ms())
-    print(json.dumps({'templates': a.templates, 'queries': a.queries, 'form': vts.scan_form(),
+    print(json.dumps({'templates': a.templates, 'queries': nb * bq, 'batches': nb, 'form': vts.scan_form(),
                       'scan_ms': float(np.mean(ms)), 'hits_correct': ok}), flush=True)
 
 
