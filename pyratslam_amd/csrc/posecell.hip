@@ -21,9 +21,11 @@
 //               reference's C order) via a packed 64-bit atomicMax.
 // max(conv(Q/t), 0) == max(conv(Q), 0)/t for t > 0, so the normalisation is
 // applied once, at the end of the step.
+#include <type_traits>
 #include <utility>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -57,6 +59,11 @@ struct PcCtlInline {     // single update(): the launch carries the control (~70
     short ioy[CTL_INLINE_MAX];
     unsigned char ifi[CTL_INLINE_MAX];
     double izf[FL];
+    // the union of the step's per-layer shifted windows (column form, whole theta
+    // extent: every block holds every layer, so it is the same for all blocks):
+    // smallest centred shifts and the union's extent in cells, formed on the host
+    // (make_ctl_inline) so the path kernel issues its window loads first thing
+    short umx, umy, uwx, uwy;
 };
 struct PcCtlRing {       // batched run(): one record per step, uploaded once per batch
     const int* ox;
@@ -1422,9 +1429,12 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
 // Window buffer of the path kernel (bytes): the whole-extent form runs one block per
 // CU, the theta-chunked form two.
 constexpr int CO_WIN_BYTES = 128 * 1024, CO_WIN_BYTES_CHUNK = 56 * 1024;
+// theta extent of the path kernel's LDS-DMA window instance (float32, whole extent,
+// control as kernel arguments): BASELINE configs[3]'s 72 layers
+constexpr int CO_DMA_TH = 72;
 
 // signed shift in (-n/2, n/2] (control shifts may exceed the grid: vtrans large)
-__device__ inline int co_centre(int o, int n) {
+__host__ __device__ inline int co_centre(int o, int n) {
     o = rs::wrapi(o, n);
     return o > n / 2 ? o - n : o;
 }
@@ -1441,12 +1451,21 @@ __device__ inline int co_wave_ext_i(int v) {
               op(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 
-template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL>
+// DMA_TH > 0: the instance for TH == DMA_TH (float32, whole extent, control as kernel
+// arguments).  Its window is an LDS image [u][v][layer] with no padding between a
+// cell's layers, so each 16-byte piece of a cell's theta run in Q has a fixed place,
+// and the pieces go global -> LDS by LDS-DMA (global_load_lds_dwordx4, lane-linear
+// 1 KiB per wave-instruction): no register staging and no ds_write (the scalar
+// stores into the odd-pitch image were 4-way bank conflicts), issued first thing from
+// the host-formed union (PcCtlInline::umx..uwy), in flight together with the
+// control's, the partials' and the filter table's loads: one round trip.
+template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL, int DMA_TH = 0>
 __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
     const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
     T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx, int gy, int KC) {
     constexpr int NT = 64 * NW, VEC = co_vec<T>();
+    constexpr bool DMA = DMA_TH > 0;
     // Q is theta-fastest, like P: the block loads the union of its layers' shifted
     // windows -- WX x WY cells, each cell's run of layers contiguous in Q -- into LDS
     // as [cell][layer] (every |shift| <= 3 at 128x128x72: 20 x 20 cells x 72 layers,
@@ -1471,6 +1490,55 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     PC_STAMP(6, 0);
+    // window strides are compile-time (the filter's LDS reads take immediate offsets):
+    // WYP cells per window row, LPC layers per cell (odd: fewer bank conflicts between
+    // lanes whose layers have different shifts; the DMA image: exactly TH), at most
+    // WXP rows
+    constexpr int WYP = TY + 2 * HALF + 6, LPC = DMA ? DMA_TH : (THM | 1), WXP = WBUF / (WYP * LPC);
+    static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
+    bool dma = false;
+    if constexpr (DMA) {
+        static_assert(sizeof(T) == 4 && !CHUNK && DMA_TH % 4 == 0 && DMA_TH <= THM, "DMA window form");
+        constexpr int PPC = DMA_TH / 4;    // 16-byte pieces per cell
+        static_assert(WXP * WYP * PPC + 63 <= WBUF / 4, "the last wave-instruction stays in the buffer");
+        const int WX = ctl.uwx, WY = ctl.uwy;
+        dma = TH == DMA_TH && WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
+        if (dma) {
+            // piece p = (u * WYP + v) * PPC + l4 lands at s_w + 4p (the padding cells
+            // v >= WY are not loaded); a thread's pieces advance by NT per instruction
+            const int ux0 = co_wrap(x0 - HALF + ctl.umx, X), uy0 = co_wrap(y0 - HALF + ctl.umy, Y);
+            const int npc = WX * WYP * PPC, wave_u = __builtin_amdgcn_readfirstlane(wave);
+            constexpr int DC = NT / PPC, DL = NT % PPC, DU = DC / WYP, DV = DC % WYP;
+            constexpr int NK = (WXP * WYP * PPC + NT - 1) / NT;
+            const int p0 = wave_u * 64 + lane;
+            int c = p0 / PPC, l4 = p0 - c * PPC, u = c / WYP, v = c - u * WYP;
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int i0 = k * NT + wave_u * 64;  // wave-uniform
+                if (i0 < npc) {
+                    if (i0 + lane < npc && v < WY) {
+                        int gr = ux0 + u, gc = uy0 + v;
+                        gr -= gr >= X ? X : 0;
+                        gc -= gc >= Y ? Y : 0;
+                        __builtin_amdgcn_global_load_lds(
+                            (__attribute__((address_space(1))) const void*)(Q + ((unsigned)gr * Y + gc) * DMA_TH + 4 * l4),
+                            (__attribute__((address_space(3))) void*)(s_w + 4 * i0), 16, 0, 0);
+                    }
+                }
+                l4 += DL;
+                v += DV;
+                u += DU;
+                if (l4 >= PPC) {
+                    l4 -= PPC;
+                    ++v;
+                }
+                if (v >= WYP) {
+                    v -= WYP;
+                    ++u;
+                }
+            }
+        }
+    }
     // The control first (its loads are the ones the first barrier waits for; clamped
     // unconditional reads, in flight together), then the normalisation partials (a
     // guarded load had its wait hoisted to the kernel's start).  Every wave forms
@@ -1508,25 +1576,33 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         const int i = tid + u * NT, fi = i / FT;
         if (i < nf * FT) s_ftab[fi * ST_FTP + (i - fi * FT)] = fr[u];
     }
+    // the DMA pieces have landed before any wave passes the barrier and reads them
+    // (a wave's waitcnt covers its own LDS-DMA; the barrier, everyone's)
+    if (DMA && dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     co_lds_barrier();
     PC_STAMP(6, 1);
-    // the union window of the block's layers (every wave reduces the shifts itself)
+    // the union window of the block's layers (every wave reduces the shifts itself;
+    // the DMA form has it from the host)
     int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
-    for (int L = lane; L < ly.nl; L += 64) {
-        mnx = min(mnx, s_ox[L]);
-        mxx = max(mxx, s_ox[L]);
-        mny = min(mny, s_oy[L]);
-        mxy = max(mxy, s_oy[L]);
+    if (DMA && dma) {
+        if constexpr (DMA) {
+            mnx = ctl.umx;
+            mny = ctl.umy;
+            mxx = mnx + ctl.uwx - (TX + 2 * HALF);
+            mxy = mny + ctl.uwy - (TY + 2 * HALF);
+        }
+    } else {
+        for (int L = lane; L < ly.nl; L += 64) {
+            mnx = min(mnx, s_ox[L]);
+            mxx = max(mxx, s_ox[L]);
+            mny = min(mny, s_oy[L]);
+            mxy = max(mxy, s_oy[L]);
+        }
+        mnx = co_wave_ext_i<false>(mnx);
+        mxx = co_wave_ext_i<true>(mxx);
+        mny = co_wave_ext_i<false>(mny);
+        mxy = co_wave_ext_i<true>(mxy);
     }
-    mnx = co_wave_ext_i<false>(mnx);
-    mxx = co_wave_ext_i<true>(mxx);
-    mny = co_wave_ext_i<false>(mny);
-    mxy = co_wave_ext_i<true>(mxy);
-    // window strides are compile-time (the filter's LDS reads take immediate offsets):
-    // WYP cells per window row, LPC layers per cell (odd: fewer bank conflicts between
-    // lanes whose layers have different shifts), at most WXP rows
-    constexpr int WYP = TY + 2 * HALF + 6, LPC = THM | 1, WXP = WBUF / (WYP * LPC);
-    static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
     const int WX = TX + 2 * HALF + mxx - mnx, WY = TY + 2 * HALF + mxy - mny;
     const bool uni = WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
     const int ux0 = co_wrap(x0 - HALF + mnx, X), uy0 = co_wrap(y0 - HALF + mny, Y);
@@ -1534,7 +1610,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
     const int nl = ly.nl;
-    if (uni && !CHUNK && TH % VEC == 0) {
+    if (DMA && dma) {
+        // the window is in LDS already
+    } else if (uni && !CHUNK && TH % VEC == 0) {
         // the common case: the union window (WX x WY cells) with 16-byte loads of VEC
         // consecutive layers of a cell, positions advanced incrementally (no
         // divisions per element); all of a thread's loads in flight together
@@ -1613,7 +1691,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
             }
         }
     }
-    co_lds_barrier();
+    if (!(DMA && dma)) co_lds_barrier();
     PC_STAMP(6, 2);
     // 7x7 filter: task (layer, column group, row part) -> TX/FS rows x CP columns of
     // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each window
@@ -2094,12 +2172,22 @@ const SepKernel<double>& sep_of<double>(const rs_pc* h) { return h->kd; }
 void make_ctl_inline(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy,
                      const int32_t* fidx, const double* zf, PcCtlInline* c) {
     const size_t b = (size_t)s * h->TH;
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
     for (int k = 0; k < h->TH; ++k) {
         c->iox[k] = (short)ox[b + k];
         c->ioy[k] = (short)oy[b + k];
         c->ifi[k] = (unsigned char)fidx[b + k];
+        const int cx = co_centre(ox[b + k], h->X), cy = co_centre(oy[b + k], h->Y);
+        mnx = std::min(mnx, cx);
+        mxx = std::max(mxx, cx);
+        mny = std::min(mny, cy);
+        mxy = std::max(mxy, cy);
     }
     for (int z = 0; z < FL; ++z) c->izf[z] = zf[(size_t)s * FL + z];
+    c->umx = (short)mnx;
+    c->umy = (short)mny;
+    c->uwx = (short)(CO_TX + 2 * HALF + mxx - mnx);
+    c->uwy = (short)(CO_TY + 2 * HALF + mxy - mny);
 }
 
 // ... or as pointers into the device ring record of step s.
@@ -2192,7 +2280,19 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
         if (!ctl) return RS_OK;
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
-        if (whole)
+        bool launched = false;
+        if constexpr (std::is_same<T, float>::value && std::is_same<CTL, PcCtlInline>::value) {
+            // TH == 72 (configs[3]): the LDS-DMA window instance
+            if (whole && h->TH == CO_DMA_TH) {
+                hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, PcCtlInline, CO_DMA_TH>),
+                                   g, dim3(64 * CO_NW), 0, h->stream, Q, static_cast<T*>(h->dP), h->dPart,
+                                   h->nPart, filt, h->nf, *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx,
+                                   h->cgy, h->coKC);
+                launched = true;
+            }
+        }
+        if (launched) {
+        } else if (whole)
             hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false, CTL>), g, dim3(64 * co_nw<T>()), 0,
                                h->stream, Q, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf,
                                *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx, h->cgy, h->coKC);
