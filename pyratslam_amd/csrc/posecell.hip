@@ -661,7 +661,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
     {
-        const T tt = (T)tot;
+        const T tt = tot != 0.0 ? T(1) / (T)tot : T(1);  // as the column form
         const int kq = wave / BX, i = wave - kq * BX;
         const int gk = k0 + kq, gi = i0 + i;
         if (gk < TH && gi < X) {
@@ -673,7 +673,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 #pragma unroll
                 for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * (T)ctl_zf(ctl, z);
                 T val = acc > T(0) ? acc : T(0);
-                if (tot != 0.0) val = val / tt;
+                val = val * tt;
                 __hip_atomic_store(&P[((size_t)gk * X + gi) * Y + j], val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
                 if constexpr (sizeof(T) == 4) {
@@ -1251,7 +1251,11 @@ __device__ inline CoLayers<CHUNK> co_layers(int ch, int KC, int TH) {
 
 // Excitation (posecell_network.py:336 -> convolution.py:228-246), inhibition
 // (:339-340) and the normalisation partial sum (:343) for one column tile.
-template <typename T, int TX, int TY, int NW, int THM, bool CHUNK>
+// FIX_TH > 0: the instance for TH == FIX_TH (the x-pass output rows then have pitch
+// TH + 64: a cell's row starts TH dwords modulo the 64 banks after the previous one, as
+// if the rows were contiguous, so the theta pass's 16-byte reads of consecutive groups
+// of consecutive cells are conflict-free)
+template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, int FIX_TH = 0>
 __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ P, T* __restrict__ Q,
                                                           double* __restrict__ part,
                                                           unsigned long long* __restrict__ res_slot,
@@ -1260,7 +1264,9 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
     constexpr int VEC = co_vec<T>();
     static_assert(TY % VEC == 0, "row vectors");
-    __shared__ __attribute__((aligned(16))) T s_in[2 * TX * TY * ((THM + 12 + 3) / 4 * 4)];  // x-pass outputs (e, i)
+    static_assert(FIX_TH == 0 || (FIX_TH == THM && !CHUNK && FIX_TH % 4 == 0), "fixed-extent instance");
+    constexpr int SPO = 4, PP = FIX_TH ? FIX_TH + 64 : (THM + 12 + 3) / 4 * 4;
+    __shared__ __attribute__((aligned(16))) T s_in[2 * TX * TY * PP];  // x-pass outputs (e, i)
     __shared__ __attribute__((aligned(16))) T s_ye[THM * HX * TY];  // [r][c][L]
     __shared__ __attribute__((aligned(16))) T s_yi[THM * HX * TY];
     __shared__ double s_red[NW];
@@ -1317,7 +1323,6 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // conflict-free).  The whole-extent form also writes each output's wrapped copy
     // (layers TH-4..TH-1 before SPO, 0..7 after SPO + TH), so every theta window is
     // one contiguous aligned run with no extra pass.
-    constexpr int SPO = 4, PP = (THM + 12 + 3) / 4 * 4;
     T* s_xe = s_in;
     T* s_xi = s_in + TX * TY * PP;
     for (int t = tid; t < ly.nl * TY; t += NT) {
@@ -1472,14 +1477,20 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // 115 KiB).  Consecutive lanes take consecutive layers: the loads read whole runs
     // of a cell's layers and the filter's LDS reads are conflict-free.  Shifts whose
     // union window does not fit take per-layer 14 x 14 windows instead.
-    constexpr int WBUF = (CHUNK ? CO_WIN_BYTES_CHUNK : CO_WIN_BYTES) / (int)sizeof(T);
+    // (the DMA instance: windows of up to 20 x 20 cells, shifts spread over at most 6
+    // cells, plus one wave-instruction of slack for the last pieces)
+    constexpr int WBUF = DMA ? 20 * (TY + 2 * HALF + 6) * DMA_TH + 4 * 64
+                             : (CHUNK ? CO_WIN_BYTES_CHUNK : CO_WIN_BYTES) / (int)sizeof(T);
     using V = typename CoVec<T>::type;
     __shared__ __attribute__((aligned(16))) T s_w[WBUF];
     // clamped 7x7 outputs [cell p][SPO + L], pitch PP (16-byte rows: the theta pass
     // reads VEC-aligned vectors); the whole-extent form also keeps wrapped copies of
     // the last 4 layers before SPO and of the first 8 after SPO + TH, so every theta
     // window is one contiguous aligned run
-    constexpr int SPO = 4, PP = (THM + 12 + 3) / 4 * 4;
+    // (the DMA instance: PP = TH + 64, so a cell's row starts TH dwords modulo the 64
+    // banks after the previous one, as if the rows were contiguous: the theta pass's
+    // 16-byte reads of consecutive groups of consecutive cells are conflict-free)
+    constexpr int SPO = 4, PP = DMA ? DMA_TH + 64 : (THM + 12 + 3) / 4 * 4;
     __shared__ __attribute__((aligned(16))) T s_p[TX * TY * PP];
     __shared__ __attribute__((aligned(16))) T s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_ox[THM], s_oy[THM], s_fo[THM];
@@ -1570,7 +1581,10 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
     for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
     tot = co_wave_sum(tot);
-    const T tt = (T)tot;
+    // the normalisation (:343-345) as a product with the reciprocal (one VALU op per
+    // output instead of a correctly rounded division; within an ulp of it); a zero
+    // total leaves the volume as it is, as the reference does
+    const T tt = tot != 0.0 ? T(1) / (T)tot : T(1);
 #pragma unroll
     for (int u = 0; u < NFR; ++u) {
         const int i = tid + u * NT, fi = i / FT;
@@ -1707,7 +1721,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
             for (int c = 0; c < CP; ++c) acc[i][c] = 0;
         const int dx = uni ? s_ox[L] - mnx : 0, dy = uni ? s_oy[L] - mny : 0;
-        const T* win = s_w + ((hf * TXH + dx) * WYP + c0 + dy) * LPC + L;
+        // the base index is opaque to the compiler, so each read keeps its compile-time
+        // offset as an immediate (ds_read2_b32 pairs) instead of an address add each
+        int wbase = ((hf * TXH + dx) * WYP + c0 + dy) * LPC + L;
+        asm volatile("" : "+v"(wbase));
+        const T* win = s_w + wbase;
 #pragma unroll
         for (int a = 0; a < TXH + 2 * HALF; ++a) {
             T w[FL + CP - 1];
@@ -1779,7 +1797,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
                 for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
                 x = x > T(0) ? x : T(0);
-                if (tot != 0.0) x = x / tt;
+                x = x * tt;
                 v[o] = x;
             }
             if (gi < X && gy < Y) {
@@ -2268,7 +2286,17 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
         const dim3 g(h->cgx * h->cgy * h->coNch);
         const bool whole = h->coKC >= h->TH;
         constexpr int THF = co_thmax<T>(), THC = co_thmax_chunk<T>();
-        if (whole)
+        bool fixed = false;
+        if constexpr (std::is_same<T, float>::value) {
+            if (whole && h->TH == CO_DMA_TH) {  // configs[3]'s theta extent
+                hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, CO_DMA_TH>), g,
+                                   dim3(64 * CO_NW), 0, h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH,
+                                   h->cgx, h->cgy, h->coKC, k);
+                fixed = true;
+            }
+        }
+        if (fixed) {
+        } else if (whole)
             hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false>), g, dim3(64 * co_nw<T>()), 0,
                                h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH, h->cgx, h->cgy,
                                h->coKC, k);
