@@ -1285,7 +1285,35 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // layer-major rows of 14 cells used a third of each line they touched).  Every
     // row of the block is in flight at once; the window never visits LDS; the y-pass
     // outputs go to LDS as [r][c][L].
-    {
+    if constexpr (FIX_TH > 0) {
+        // the fixed-extent instance: 16-byte loads of 4 consecutive layers of a cell
+        // (a quarter of the load instructions), task (row r, half h of the row's
+        // outputs, layer group g): 10 window cells, 4 outputs x 4 layers, each output
+        // one 16-byte LDS store; 14 x 2 x TH/4 tasks (504 at TH = 72: 8 waves)
+        constexpr int NG = FIX_TH / 4, TH2 = TY / 2, HW = TH2 + 2 * HALF;
+        static_assert(HX * 2 * NG <= NT, "one task per thread");
+        const int t = tid;
+        if (t < HX * 2 * NG) {
+            const int r = t / (2 * NG), rem = t - r * (2 * NG), h = rem / NG, g = rem - h * NG;
+            const T* rowp = P + ((size_t)co_wrap(x0 - HALF + r, X) * Y) * FIX_TH + 4 * g;
+            V w[HW];
+#pragma unroll
+            for (int c = 0; c < HW; ++c)
+                w[c] = *reinterpret_cast<const V*>(rowp + (size_t)co_wrap(y0 - HALF + h * TH2 + c, Y) * FIX_TH);
+#pragma unroll
+            for (int c = 0; c < TH2; ++c) {
+                V e = {0, 0, 0, 0}, gg = {0, 0, 0, 0};
+#pragma unroll
+                for (int q = 0; q < FL; ++q) {
+                    e += k.ge[q] * w[c + q];
+                    gg += k.gi[q] * w[c + q];
+                }
+                const int o = (r * TY + h * TH2 + c) * THM + 4 * g;
+                *reinterpret_cast<V*>(s_ye + o) = e;
+                *reinterpret_cast<V*>(s_yi + o) = gg;
+            }
+        }
+    } else {
         constexpr int NR = (THM * HX + NT - 1) / NT;
         const int nrow = ly.nl * HX;
         T w[NR][HY];
