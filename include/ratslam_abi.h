@@ -77,6 +77,10 @@ int rs_device_count(void);
 int rs_dev_malloc(int device, size_t bytes, void** ptr);
 int rs_dev_free(void* ptr);
 int rs_dev_copy(void* dst, const void* src, size_t bytes);
+/* pinned, GPU-visible host memory (hipHostMalloc, mapped + coherent): the target of
+ * rs_pc_read_pinned, so the .posecells readback needs no host-side copy */
+int rs_host_alloc(size_t bytes, void** ptr);
+int rs_host_free(void* ptr);
 
 /* ------------------------------------------------------------------------ */
 /* Pose-cell network                                                         */
@@ -149,6 +153,10 @@ int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th);
 int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]);
 /* whole volume as float64, C order (X, Y, TH) -- the reference's .posecells */
 int rs_pc_read(rs_pc* h, double* host_xyth);
+/* the same volume written by the GPU straight into pinned host memory from
+ * rs_host_alloc (at least X*Y*TH doubles): one launch and a sync, no host copy --
+ * the drop-in .posecells readback the ROS node pays every step (ros_simulate.py:140,145) */
+int rs_pc_read_pinned(rs_pc* h, double* pinned_xyth);
 int rs_pc_write(rs_pc* h, const double* host_xyth);
 /* sum of all cells (float64 accumulation) */
 int rs_pc_total(rs_pc* h, double* total);

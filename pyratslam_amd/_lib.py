@@ -63,6 +63,8 @@ SIGNATURES = {
     'rs_dev_malloc': (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     'rs_dev_free': (ctypes.c_int, [_vp]),
     'rs_dev_copy': (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    'rs_host_alloc': (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    'rs_host_free': (ctypes.c_int, [_vp]),
     'rs_pc_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(PcParams), ctypes.c_int, ctypes.POINTER(_vp)]),
     'rs_pc_destroy': (ctypes.c_int, [_vp]),
@@ -82,6 +84,7 @@ SIGNATURES = {
     'rs_pc_inject': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     'rs_pc_get_max': (ctypes.c_int, [_vp, _i32p]),
     'rs_pc_read': (ctypes.c_int, [_vp, _f64p]),
+    'rs_pc_read_pinned': (ctypes.c_int, [_vp, _vp]),
     'rs_pc_write': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_total': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_last_ms': (ctypes.c_int, [_vp, _f64p]),

@@ -2033,6 +2033,25 @@ __global__ void pc_export_kernel(const T* __restrict__ P, double* __restrict__ o
         out[e] = (double)P[thfast ? e : pc_layer_major(e, X, Y, TH)];
 }
 
+// The same export with 16-byte stores (two consecutive cells per thread): a wave's
+// stores are 1 KiB contiguous, the unit host writes over PCIe favour.  out is
+// 16-byte aligned (rs_host_alloc / hipMalloc); an odd last cell goes alone.
+template <typename T>
+__global__ void pc_export2_kernel(const T* __restrict__ P, double* __restrict__ out, int X, int Y,
+                                  int TH, int thfast) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const size_t n = (size_t)X * Y * TH, n2 = n / 2;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t e = 2 * i;
+        d2 v;
+        v.x = (double)P[thfast ? e : pc_layer_major(e, X, Y, TH)];
+        v.y = (double)P[thfast ? e + 1 : pc_layer_major(e + 1, X, Y, TH)];
+        *reinterpret_cast<d2*>(out + e) = v;
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
+        out[n - 1] = (double)P[thfast ? n - 1 : pc_layer_major(n - 1, X, Y, TH)];
+}
+
 template <typename T>
 __global__ void pc_import_kernel(const double* __restrict__ in, T* __restrict__ P, int X, int Y,
                                  int TH, int thfast) {
@@ -3046,6 +3065,25 @@ int rs_pc_read(rs_pc* h, double* host) {
     if (dma) RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     if (!dma) std::memcpy(host, h->hRead, sizeof(double) * h->n);
+    return RS_OK;
+}
+
+int rs_pc_read_pinned(rs_pc* h, double* pinned) {
+    rs::clear_error();
+    RS_CHECK(h && pinned, RS_ERR_ARG, "null argument");
+    RS_CHECK(reinterpret_cast<uintptr_t>(pinned) % 16 == 0, RS_ERR_ARG, "pinned buffer not 16-byte aligned");
+    RS_HIP(hipSetDevice(h->device));
+    double* dst = nullptr;
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), pinned, 0));
+    const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+    else
+        hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+    RS_HIP(hipGetLastError());
+    RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
 }
 

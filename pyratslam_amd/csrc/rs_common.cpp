@@ -52,4 +52,18 @@ int rs_dev_copy(void* dst, const void* src, size_t bytes) {
     return RS_OK;
 }
 
+int rs_host_alloc(size_t bytes, void** ptr) {
+    rs::clear_error();
+    RS_CHECK(ptr, RS_ERR_ARG, "null output pointer");
+    *ptr = nullptr;
+    RS_HIP(hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    return RS_OK;
+}
+
+int rs_host_free(void* ptr) {
+    rs::clear_error();
+    if (ptr) RS_HIP(hipHostFree(ptr));
+    return RS_OK;
+}
+
 }  // extern "C"

@@ -15,6 +15,7 @@ volume work runs in ``pc_excite`` + ``pc_path`` (``csrc/posecell.hip``).
 import ctypes
 import math
 import threading
+import weakref
 
 import numpy as np
 
@@ -33,6 +34,46 @@ PC_C_SIZE_TH = 2.0 * np.pi / PC_DIM_TH
 
 _PRECISIONS = {'float32': _lib.RS_PREC_F32, np.float32: _lib.RS_PREC_F32,
                'float64': _lib.RS_PREC_F64, np.float64: _lib.RS_PREC_F64}
+
+
+class _PinnedArrays:
+    """Float64 arrays in pinned, GPU-visible host memory (rs_host_alloc), handed out
+    one per ``.posecells`` read: the GPU writes the volume straight into the array
+    the caller gets (rs_pc_read_pinned), so the readback needs no host-side copy.
+    Each array owns its block until it is garbage-collected, when the block goes
+    back to the free list (the caller's arrays never alias one another)."""
+
+    def __init__(self, lib, n):
+        self._lib, self._n = lib, n
+        self._free = []
+        self._lock = threading.Lock()
+
+    def array(self, shape):
+        with self._lock:
+            ptr = self._free.pop() if self._free else None
+        if ptr is None:
+            p = ctypes.c_void_p()
+            _lib.check(self._lib.rs_host_alloc(8 * self._n, ctypes.byref(p)))
+            ptr = p.value
+        view = (ctypes.c_double * self._n).from_address(ptr)
+        weakref.finalize(view, self._release, ptr).atexit = False  # the process frees it at exit
+        return np.frombuffer(view, dtype=np.float64).reshape(shape), ptr
+
+    def _release(self, ptr):
+        with self._lock:
+            if not self._closed:
+                self._free.append(ptr)
+                return
+        self._lib.rs_host_free(ctypes.c_void_p(ptr))  # an array that outlived its network
+
+    _closed = False
+
+    def close(self):
+        with self._lock:
+            self._closed = True
+            free, self._free = self._free, []
+        for ptr in free:
+            self._lib.rs_host_free(ctypes.c_void_p(ptr))
 
 
 def round_up(x):  # posecell_network.py:19-20
@@ -64,6 +105,7 @@ class PoseCellNetwork:
         self._max_valid = False
         self._mutex = threading.Lock()
         self._h = None
+        self._pinned = None
         self._lib = _lib.require_device()
         ge, gi, scale = F.separable_factors()
         self._table = np.ascontiguousarray(self.filter_table.filters, dtype=np.float64)
@@ -100,6 +142,9 @@ class PoseCellNetwork:
         if self._h is not None and self._h.value:
             self._lib.rs_pc_destroy(self._h)
         self._h = None
+        if getattr(self, '_pinned', None) is not None:
+            self._pinned.close()
+            self._pinned = None
 
     def __del__(self):
         try:
@@ -116,10 +161,15 @@ class PoseCellNetwork:
     # -- state ------------------------------------------------------------------
     @property
     def posecells(self):
-        """Copy of the activity volume, float64 C order (X, Y, TH) (posecell_network.py:27)."""
-        out = np.empty(self.shape, dtype=np.float64)
+        """Copy of the activity volume, float64 C order (X, Y, TH) (posecell_network.py:27).
+
+        The GPU writes it straight into a fresh pinned host array (no host-side copy;
+        ros_simulate.py:140,145 reads it after every update)."""
         with self._mutex:
-            _lib.check(self._lib.rs_pc_read(self._h, _lib.ptr(out, ctypes.c_double)))
+            if self._pinned is None:
+                self._pinned = _PinnedArrays(self._lib, int(np.prod(self.shape)))
+            out, ptr = self._pinned.array(self.shape)
+            _lib.check(self._lib.rs_pc_read_pinned(self._h, ctypes.c_void_p(ptr)))
         return out
 
     @posecells.setter

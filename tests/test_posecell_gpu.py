@@ -394,3 +394,39 @@ def test_library_control_matches_host_control(pcn, shape):
     assert np.array_equal(e.run(od[15:25]), f._run_host_control(np.ascontiguousarray(od[15:25])))
     assert e.posecells.tobytes() == f.posecells.tobytes()
     assert e.run(np.zeros((0, 2))).shape == (0, 3)
+
+
+@pytest.mark.parametrize('precision', ['float32', 'float64'])
+def test_posecells_pinned_readback_arrays_are_independent(pcn, precision):
+    """.posecells is written by the GPU straight into a pinned host array
+    (rs_pc_read_pinned): each read returns its own array, equal to the copying
+    readback (rs_pc_read), unchanged by later steps and reads, across pool reuse
+    and an odd cell count."""
+    import ctypes
+    from pyratslam_amd import _lib
+    for shape in ((32, 32, 18), (13, 11, 7)):
+        net = pcn(shape, precision=precision)
+        ref = P.PoseCellOracle(shape)
+        loc = tuple(s // 2 for s in shape)
+        net.inject(1, loc)
+        ref.inject(1, loc)
+        od = odometry(12, 7)
+        kept = []
+        for s, v in enumerate(od):
+            net.update(v)
+            ref.update(v)
+            a = net.posecells
+            b = np.empty(shape, dtype=np.float64)
+            _lib.check(net._lib.rs_pc_read(net._h, _lib.ptr(b, ctypes.c_double)))
+            assert a.dtype == np.float64 and a.shape == shape and a.flags.c_contiguous
+            assert np.array_equal(a, b)
+            tol = F32_TOL if precision == 'float32' else F64_TOL
+            assert np.abs(a - ref.posecells).max() < tol
+            if s % 3 == 0:
+                kept.append((a, a.copy()))      # held across later steps
+            del a                               # the others go back to the pool
+        for a, snap in kept:
+            assert np.array_equal(a, snap)
+        net.close()
+        for a, snap in kept:                    # arrays outlive their network
+            assert np.array_equal(a, snap)
