@@ -428,12 +428,27 @@ def bench_node_step(args, d):
         r1 = time.perf_counter()
         assert p.shape == shape
         net.close()
+        # readback='eager': update() exports the new volume before its one sync
+        eg = PoseCellNetwork(shape, device=d.dev, readback='eager')
+        eg.inject(1, tuple(s // 2 for s in shape))
+        for v in od[:32]:
+            eg.update(v)
+            eg.posecells
+        e0 = time.perf_counter()
+        for v in od[32:32 + n]:
+            eg.update(v)
+            p = eg.posecells
+        e1 = time.perf_counter()
+        eg.close()
         out['x'.join(map(str, shape))] = {
             'update_us': 1e6 * (t1 - t0) / n, 'update_plus_read_us': 1e6 * (t2 - t1) / n,
             'read_us': 1e6 * (r1 - r0) / n, 'node_steps_per_s': n / (t2 - t1),
+            'update_plus_read_eager_us': 1e6 * (e1 - e0) / n, 'node_steps_per_s_eager': n / (e1 - e0),
             'read_bytes': 8 * shape[0] * shape[1] * shape[2]}
-    out['note'] = ('update() then `.posecells` (float64, C order, a fresh array per read) per '
-                   'step, one host round trip each, as ros_simulate.py:134-145 does')
+    out['note'] = ('update() then `.posecells` (float64, C order, a fresh array per read, written '
+                   'by the GPU straight into pinned host memory) per step, as ros_simulate.py:134-145 '
+                   'does; _eager: PoseCellNetwork(readback="eager"), the export queued inside '
+                   'update() before its one host sync')
     return out
 
 
@@ -557,7 +572,23 @@ def bench_replay(args, d):
     r.replay_events(events)
     dt = d.max(time.perf_counter() - t0)
     res = r.results()
-    return {'messages': len(events), 'updates': int(len(res['pc_max'])), 'reduce': reduce_kind,
+    # the node's per-step work in full: every update also reads the whole .posecells
+    # volume (ros_simulate.py:140-145 publishes it), steps one by one
+    # (one rank: the pose cells are replicated, so each rank's node work is this)
+    publish = None
+    if d.world == 1:
+        rp = replay.RatslamReplay(device=d.dev, publish=True)
+        p0 = time.perf_counter()
+        rp.replay_events(events)
+        dtp = time.perf_counter() - p0
+        resp = rp.results()
+        assert [tuple(m) for m in resp['pc_max']] == [tuple(m) for m in res['pc_max']]
+        publish = {'messages_per_s': len(events) / dtp, 'seconds': dtp,
+                   'posecells_values_read_per_update': rp.published // max(1, len(resp['pc_max'])),
+                   'note': 'per update also the .posecells read the node publishes '
+                           '(PoseCellNetwork readback="eager"), steps one by one'}
+    return {'publish': publish,
+            'messages': len(events), 'updates': int(len(res['pc_max'])), 'reduce': reduce_kind,
             'frames': int(len(res['template_index'])), 'templates': int(res['templates']),
             'seconds': dt, 'messages_per_s': len(events) / dt,
             'updates_per_s': len(res['pc_max']) / dt, 'frames_per_s': len(res['template_index']) / dt,

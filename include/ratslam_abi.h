@@ -144,6 +144,12 @@ int rs_pc_odom_control(int TH, double vtrans_scale, double vrot_scale, const dou
                        int zorig_min, int nz, const double* zf_table, int n, const double* odom,
                        int32_t* ox, int32_t* oy, int32_t* fidx, double* zf, int32_t* status);
 int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* first_bad);
+/* rs_pc_update_odom followed, on the same stream and before its one host sync, by the
+ * export of the new volume into pinned memory from rs_host_alloc (as
+ * rs_pc_read_pinned): update() and the .posecells read the ROS node makes after every
+ * step (ros_simulate.py:134-145) as one round trip.  On an error the volume export
+ * may not have run. */
+int rs_pc_update_odom_read(rs_pc* h, double vtrans, double vrot, int32_t out_xyz[3], double* pinned_xyth);
 /* steps 1-4 of update() alone (excitation, global inhibition, normalisation):
  * the state the reference leaves behind when path_integration raises KeyError */
 int rs_pc_excite(rs_pc* h);

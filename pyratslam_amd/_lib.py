@@ -85,6 +85,7 @@ SIGNATURES = {
     'rs_pc_get_max': (ctypes.c_int, [_vp, _i32p]),
     'rs_pc_read': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_read_pinned': (ctypes.c_int, [_vp, _vp]),
+    'rs_pc_update_odom_read': (ctypes.c_int, [_vp, ctypes.c_double, ctypes.c_double, _i32p, _vp]),
     'rs_pc_write': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_total': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_last_ms': (ctypes.c_int, [_vp, _f64p]),

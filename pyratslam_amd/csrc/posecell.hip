@@ -2144,6 +2144,7 @@ struct rs_pc {
     std::vector<int32_t> cOx, cOy, cRows;
     std::vector<double> cZf;
     bool dbgSkipExport = false;  // rs_pc_debug(RS_PC_DBG_SKIP_EXPORT): the next run leaves hRes unwritten
+    double* exportDev = nullptr;  // rs_pc_update_odom_read: the state export queued behind the step
     double* hRead = nullptr;     // rs_pc_read: pinned float64 volume the export kernel writes in place
     double* hReadDev = nullptr;
 };
@@ -2477,6 +2478,16 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         RS_HIP(hipGetLastError());
     }
     h->dbgSkipExport = false;
+    if (h->exportDev) {  // the volume after the last step, into the caller's pinned array
+        const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
+        if (h->prec == RS_PREC_F32)
+            hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
+                               static_cast<const float*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)h->cols);
+        else
+            hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
+                               static_cast<const double*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)h->cols);
+        RS_HIP(hipGetLastError());
+    }
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
     for (int s = 0; s < n; ++s)
@@ -2975,6 +2986,17 @@ int rs_pc_update_odom(rs_pc* h, double vtrans, double vrot, int32_t out_xyz[3]) 
     }
     RS_CHECK(st == RS_OK, st, "odometry (%g, %g) outside the control tables", vtrans, vrot);
     return pc_run_impl(h, 1, h->cOx.data(), h->cOy.data(), h->cRows.data(), h->cZf.data(), out_xyz);
+}
+
+int rs_pc_update_odom_read(rs_pc* h, double vtrans, double vrot, int32_t out_xyz[3], double* pinned) {
+    rs::clear_error();
+    RS_CHECK(h && pinned, RS_ERR_ARG, "null argument");
+    RS_CHECK(reinterpret_cast<uintptr_t>(pinned) % 16 == 0, RS_ERR_ARG, "pinned buffer not 16-byte aligned");
+    RS_HIP(hipSetDevice(h->device));
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->exportDev), pinned, 0));
+    const int st = rs_pc_update_odom(h, vtrans, vrot, out_xyz);
+    h->exportDev = nullptr;
+    return st;
 }
 
 int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* first_bad) {

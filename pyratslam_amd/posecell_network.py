@@ -84,11 +84,19 @@ class PoseCellNetwork:
     """Continuous-attractor pose-cell network on one GPU.
 
     ``precision``: 'float32' (default; activations within 1e-5 of the float64
-    reference) or 'float64'.  ``device``: HIP device ordinal.
+    reference) or 'float64'.  ``device``: HIP device ordinal.  ``readback``: 'lazy'
+    (default: ``.posecells`` exports the volume when read) or 'eager' (every
+    ``update()`` also exports the new volume into a pinned array before its one host
+    sync, and the next ``.posecells`` read returns that array: the ROS node's
+    update-then-publish step, ros_simulate.py:134-145, as one round trip).
     Extra keyword arguments are accepted and ignored, like the reference (:24).
     """
 
-    def __init__(self, shape, precision='float32', device=0, **kwargs):
+    def __init__(self, shape, precision='float32', device=0, readback='lazy', **kwargs):
+        if readback not in ('lazy', 'eager'):
+            raise ValueError("readback must be 'lazy' or 'eager', got %r" % (readback,))
+        self._eager = readback == 'eager'
+        self._fresh = None   # eager: the volume exported by the last update()
         if len(shape) != 3:
             raise TypeError('PoseCellNetwork shape must be (X, Y, TH), got %r' % (shape,))
         self.shape = tuple(int(s) for s in shape)
@@ -131,6 +139,9 @@ class PoseCellNetwork:
         self._update_odom = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
                                              ctypes.c_double, ctypes.c_void_p)(
             ('rs_pc_update_odom', self._lib))
+        self._update_odom_read = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_double,
+                                                  ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p)(
+            ('rs_pc_update_odom_read', self._lib))
 
     def _upload_odometry_tables(self):
         """Tables for the library-side control of update()/run() (filters.odometry_tables)."""
@@ -166,11 +177,17 @@ class PoseCellNetwork:
         The GPU writes it straight into a fresh pinned host array (no host-side copy;
         ros_simulate.py:140,145 reads it after every update)."""
         with self._mutex:
-            if self._pinned is None:
-                self._pinned = _PinnedArrays(self._lib, int(np.prod(self.shape)))
-            out, ptr = self._pinned.array(self.shape)
+            if self._fresh is not None:   # exported by the last update() (readback='eager')
+                out, self._fresh = self._fresh, None
+                return out
+            out, ptr = self._pinned_array()
             _lib.check(self._lib.rs_pc_read_pinned(self._h, ctypes.c_void_p(ptr)))
         return out
+
+    def _pinned_array(self):
+        if self._pinned is None:
+            self._pinned = _PinnedArrays(self._lib, int(np.prod(self.shape)))
+        return self._pinned.array(self.shape)
 
     @posecells.setter
     def posecells(self, value):
@@ -179,6 +196,7 @@ class PoseCellNetwork:
             raise TypeError('posecells must have shape %r, got %r' % (self.shape, v.shape))
         v = np.ascontiguousarray(v, dtype=np.float64)
         with self._mutex:
+            self._fresh = None
             _lib.check(self._lib.rs_pc_write(self._h, _lib.ptr(v, ctypes.c_double)))
             self._max_valid = False
 
@@ -201,6 +219,7 @@ class PoseCellNetwork:
         if not (0 <= x < X and 0 <= y < Y and 0 <= th < TH):
             raise IndexError('inject location %r outside grid %r' % (loc, self.shape))
         with self._mutex:
+            self._fresh = None
             _lib.check(self._lib.rs_pc_inject(self._h, float(energy), x, y, th))
             self._max_valid = False
 
@@ -221,7 +240,14 @@ class PoseCellNetwork:
         vtrans, vrot = float(v[0]), float(v[1])
         out = self._out3
         with self._mutex:
-            st = self._update_odom(self._h, vtrans, vrot, self._out3_addr)
+            self._fresh = None
+            if self._eager:
+                arr, ptr = self._pinned_array()
+                st = self._update_odom_read(self._h, vtrans, vrot, self._out3_addr, ptr)
+                if st == _lib.RS_OK:
+                    self._fresh = arr
+            else:
+                st = self._update_odom(self._h, vtrans, vrot, self._out3_addr)
             if st == _lib.RS_OK:
                 self.max_pc = (int(out[0]), int(out[1]), int(out[2]))
                 self._max_valid = True
@@ -269,6 +295,7 @@ class PoseCellNetwork:
         out = np.empty((n, 3), dtype=np.int32)
         bad = ctypes.c_int(-1)
         with self._mutex:
+            self._fresh = None
             st = self._lib.rs_pc_run_odom(self._h, n, _lib.ptr(od, ctypes.c_double),
                                           _lib.ptr(out, ctypes.c_int32), ctypes.byref(bad))
             if st in (_lib.RS_OK, _lib.RS_ERR_LUT_KEY):

@@ -65,10 +65,15 @@ class RatslamReplay:
     def __init__(self, pose_size=POSE_SIZE, im_size=IM_SIZE, x_range=X_RANGE, y_range=Y_RANGE,
                  x_step=X_STEP, y_step=Y_STEP, match_threshold=MATCH_THRESHOLD,
                  odom_freq=ODOM_FREQ, feedback_energy=None, pcn=None, vts=None, em=None,
-                 device=0, precision='float32', batch=True):
+                 device=0, precision='float32', batch=True, publish=False):
+        # publish: the node's per-step work in full -- every update reads the whole
+        # .posecells volume, as ros_simulate.py:140-145 does to publish it -- so steps
+        # go one by one (no batched run()) and the network exports eagerly
+        self.publish = publish
         if pcn is None:
             from .posecell_network import PoseCellNetwork
-            pcn = PoseCellNetwork(shape=pose_size, precision=precision, device=device)
+            pcn = PoseCellNetwork(shape=pose_size, precision=precision, device=device,
+                                  readback='eager' if publish else 'lazy')
         if vts is None:
             from .view_templates import ViewTemplates
             vts = ViewTemplates(x_range=x_range, y_range=y_range, x_step=x_step, y_step=y_step,
@@ -78,7 +83,8 @@ class RatslamReplay:
         self.em = em if em is not None else ExperienceMap()
         self.odom_freq = odom_freq
         self.feedback_energy = feedback_energy
-        self.batch = batch and hasattr(pcn, 'run')
+        self.batch = batch and hasattr(pcn, 'run') and not publish
+        self.published = 0   # .posecells volumes read (publish=True)
         self.twist_data = deque()
         # ros_simulate.py:56-57 (Python-2 int / 2, then math.floor)
         self.pcn.inject(1, tuple(int(math.floor(s // 2)) for s in pose_size))
@@ -99,9 +105,13 @@ class RatslamReplay:
             self.pcn.inject(self.feedback_energy, tuple(template_match.location()))
 
     def update_posecells(self, vtrans, vrot):
-        """ros_simulate.py:134-146 (publishing reduced to recording)."""
+        """ros_simulate.py:134-146 (publishing reduced to recording; with publish=True
+        the volume is read as the node reads it to publish, :140)."""
         self.pcn.update((vtrans, vrot))
         self._record(vtrans, vrot, self.pcn.get_pc_max())
+        if self.publish:
+            pc = self.pcn.posecells
+            self.published += pc.size
 
     def _record(self, vtrans, vrot, pc_max):
         pc_max = tuple(int(v) for v in pc_max)

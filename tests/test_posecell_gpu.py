@@ -430,3 +430,29 @@ def test_posecells_pinned_readback_arrays_are_independent(pcn, precision):
         net.close()
         for a, snap in kept:                    # arrays outlive their network
             assert np.array_equal(a, snap)
+
+
+def test_eager_readback_equals_lazy(pcn):
+    """readback='eager': update() exports the new volume before its one sync and the
+    next .posecells returns it; identical to the lazy readback after every update,
+    after inject (the export is invalidated), after run() and with repeated reads."""
+    shape = (32, 32, 18)
+    a, b = pcn(shape), pcn(shape, readback='eager')
+    for n in (a, b):
+        n.inject(1, (16, 16, 9))
+    od = odometry(20, 13)
+    for s, v in enumerate(od[:12]):
+        assert a.update(v) == b.update(v)
+        pb = b.posecells
+        assert np.array_equal(a.posecells, pb)
+        assert np.array_equal(b.posecells, pb)        # a second read: a fresh export
+        if s == 5:
+            for n in (a, b):
+                n.inject(0.5, (3, 4, 5))
+            assert np.array_equal(a.posecells, b.posecells)
+    b.update(od[12])
+    a.update(od[12])
+    assert np.array_equal(a.run(od[13:]), b.run(od[13:]))
+    assert np.array_equal(a.posecells, b.posecells)  # run() invalidated the export
+    with pytest.raises(ValueError):
+        pcn(shape, readback='sometimes')

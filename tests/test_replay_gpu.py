@@ -23,10 +23,14 @@ def _events(golden):
     return synthetic.ros_stream(int(golden['n']), seed=int(golden['seed']))
 
 
-@pytest.mark.parametrize('batch', [True, False])
-def test_gpu_replay_matches_reference(golden, batch):
+@pytest.mark.parametrize('batch,publish', [(True, False), (False, False), (False, True)])
+def test_gpu_replay_matches_reference(golden, batch, publish):
+    """publish=True: every update also reads .posecells (the node's publish,
+    ros_simulate.py:140-145) through the eager readback."""
     from pyratslam_amd import replay
-    r = replay.RatslamReplay(batch=batch).replay_events(_events(golden))
+    r = replay.RatslamReplay(batch=batch, publish=publish).replay_events(_events(golden))
+    if publish:
+        assert r.published == len(r.pc_max) * int(np.prod(replay.POSE_SIZE))
     res = r.results()
     assert np.array_equal(res['pc_max'], golden['pc_max'])
     assert np.array_equal(res['template_index'], golden['template_index'])

@@ -23,6 +23,17 @@ for shape in ((21, 21, 36), (64, 64, 36)):
         return buf.copy()
 
     res = {}
+    eager = PoseCellNetwork(shape, readback='eager')
+    eager.inject(1, tuple(s // 2 for s in shape))
+    for v in od[:100]:
+        eager.update(v)
+        eager.posecells
+    t0 = time.perf_counter()
+    for v in od[100:1100]:
+        eager.update(v)
+        eager.posecells
+    res['eager'] = {'update_plus_read_us': round(1e3 * (time.perf_counter() - t0), 2)}
+    eager.close()
     for name, read in (('pinned', lambda: net.posecells), ('copying', copying)):
         for v in od[:100]:
             net.update(v)
