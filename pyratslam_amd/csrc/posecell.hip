@@ -1754,22 +1754,33 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         int wbase = ((hf * TXH + dx) * WYP + c0 + dy) * LPC + L;
         asm volatile("" : "+v"(wbase));
         const T* win = s_w + wbase;
+        // the window rows in a rotated order per wave group (waves w, w+4, w+8 share a
+        // SIMD): the groups' LDS read bursts and FMA runs interleave instead of
+        // running in lockstep behind the barrier
+        auto rows = [&](auto rot_c) __attribute__((always_inline)) {
+            constexpr int ROT = decltype(rot_c)::value, NRW = TXH + 2 * HALF;
 #pragma unroll
-        for (int a = 0; a < TXH + 2 * HALF; ++a) {
-            T w[FL + CP - 1];
+            for (int aa = 0; aa < NRW; ++aa) {
+                const int a = (aa + ROT) % NRW;
+                T w[FL + CP - 1];
 #pragma unroll
-            for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WYP + q) * LPC];
-            if (a % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WYP + q) * LPC];
+                if (aa % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < TXH; ++i) {
-                const int x = a - i;
-                if (x < 0 || x >= FL) continue;
+                for (int i = 0; i < TXH; ++i) {
+                    const int x = a - i;
+                    if (x < 0 || x >= FL) continue;
 #pragma unroll
-                for (int c = 0; c < CP; ++c)
+                    for (int c = 0; c < CP; ++c)
 #pragma unroll
-                    for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
+                        for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
+                }
             }
-        }
+        };
+        const int grp = __builtin_amdgcn_readfirstlane(tid >> 8);  // wave / 4
+        if (grp == 0) rows(std::integral_constant<int, 0>{});
+        else if (grp == 1) rows(std::integral_constant<int, 3>{});
+        else rows(std::integral_constant<int, 6>{});
         // with the wrapped copies of the whole-extent form (layers TH-4..TH-1 also
         // before SPO, 0..7 also after SPO + TH; TH >= 10, so at most one of each)
         const int Lw1 = !CHUNK && L < 8 ? nl + L : INT_MIN, Lw2 = !CHUNK && L >= nl - 4 ? L - nl : INT_MIN;
