@@ -456,3 +456,27 @@ def test_eager_readback_equals_lazy(pcn):
     assert np.array_equal(a.posecells, b.posecells)  # run() invalidated the export
     with pytest.raises(ValueError):
         pcn(shape, readback='sometimes')
+
+
+@pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
+def test_large_grid_wide_shifts_vs_c_oracle(pcn, precision, tol):
+    """128x128x72 (the column form's TH = 72 instances): steps whose shifted windows'
+    union fits the LDS-DMA image (|shift| <= 3) mixed with fast ones (vtrans up to
+    2 m: shifts up to 10 cells, the per-layer-window fallback), and a step that
+    turns the heading by more than a layer, against the C oracle step by step."""
+    from oracle import c_oracle as C
+    shape = (128, 128, 72)
+    r = np.random.default_rng(23)
+    n = 12
+    od = np.stack([np.where(r.random(n) < 0.5, r.uniform(0, 0.6, n), r.uniform(0.9, 2.0, n)),
+                   r.uniform(-0.15, 0.15, n)], axis=1)
+    od[5, 1] = 0.2
+    net = pcn(shape, precision=precision)
+    assert net.step_form() == 'cols'
+    ref = C.PoseCellC(shape)
+    for x in (net, ref):
+        x.inject(1, (64, 64, 36))
+    for s, v in enumerate(od):
+        m = ref.update(v)
+        assert net.update(v) == m, (s, v)
+    assert np.abs(net.posecells - ref.posecells).max() < tol
