@@ -40,6 +40,9 @@ def find(d, pattern):
 
 
 def trace_stats(d):
+    """Per kernel: rocprofv3's --stats summary, plus the median over the per-dispatch
+    kernel trace (the first dispatches of a process run while the clocks ramp up, which
+    pulls the average above the steady state the bench's timed steps see)."""
     f = find(d, '*kernel_stats.csv')
     out = {}
     if not f:
@@ -48,6 +51,15 @@ def trace_stats(d):
         out[short(r['Name'])] = {'calls': int(r['Calls']), 'avg_us': float(r['AverageNs']) / 1e3,
                                  'min_us': float(r['MinNs']) / 1e3, 'max_us': float(r['MaxNs']) / 1e3,
                                  'pct': float(r['Percentage'])}
+    t = find(d, '*kernel_trace.csv')
+    if t:
+        per = collections.defaultdict(list)
+        for r in csv.DictReader(open(t)):
+            per[short(r['Kernel_Name'])].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+        for k, v in per.items():
+            if k in out:
+                v.sort()
+                out[k]['median_us'] = v[len(v) // 2]
     return out
 
 
@@ -102,7 +114,8 @@ def traffic_of(configs, tag):
             e = ks[k]
             traffic['scans'][c] = {
                 'kernel': k, 'templates_per_launch': SCANS[c][0], 'queries': SCANS[c][1],
-                'kernel_us_rocprof': e['trace']['avg_us'],
+                'kernel_us_rocprof': e['trace'].get('median_us', e['trace']['avg_us']),
+                'kernel_us_rocprof_avg': e['trace']['avg_us'],
                 'valu_insts_per_launch': e.get('sq', {}).get('SQ_INSTS_VALU'),
                 'hbm_bytes_per_launch': e.get('hbm_bytes_per_dispatch'),
                 'wave_cycle_split': e.get('wave_cycle_split'),
@@ -118,7 +131,8 @@ def traffic_of(configs, tag):
             hb = [ks[n].get('hbm_bytes_per_dispatch') for n in (ex, pa)]
             traffic['pose_cell'][form] = {
                 'shape': shape, 'kernels': [ex, pa],
-                'kernel_us_rocprof': {'excite': ks[ex]['trace']['avg_us'], 'path': ks[pa]['trace']['avg_us']},
+                'kernel_us_rocprof': {'excite': ks[ex]['trace'].get('median_us', ks[ex]['trace']['avg_us']),
+                                      'path': ks[pa]['trace'].get('median_us', ks[pa]['trace']['avg_us'])},
                 'hbm_bytes_per_step': sum(hb) if all(hb) else None,
                 'source': f'{tag}_pmc_summary.json'}
     return traffic
@@ -152,6 +166,13 @@ def main():
         f = find(os.path.join(a.dir, c + '_trace'), '*kernel_stats.csv')
         if f:
             shutil.copy(f, os.path.join(raw, f'{c}_kernel_stats.csv'))
+        t = find(os.path.join(a.dir, c + '_trace'), '*kernel_trace.csv')
+        if t:  # per dispatch: name, start, end (the medians' input)
+            with open(t) as src, open(os.path.join(raw, f'{c}_kernel_trace.csv'), 'w', newline='') as dst:
+                wr = csv.writer(dst)
+                wr.writerow(['Kernel_Name', 'Start_Timestamp', 'End_Timestamp'])
+                for r in csv.DictReader(src):
+                    wr.writerow([short(r['Kernel_Name']), r['Start_Timestamp'], r['End_Timestamp']])
         with open(os.path.join(raw, f'{c}_counters.csv'), 'w', newline='') as fh:
             wr = csv.writer(fh)
             wr.writerow(['pass', 'kernel', 'counter', 'dispatches', 'mean_value'])
@@ -164,7 +185,8 @@ def main():
         shutil.copy(f, os.path.join(raw, 'bench_kernel_stats.csv'))
     for c, rec in list(traffic['scans'].items()) + list(traffic['pose_cell'].items()):
         cfg = c if c in SCANS else {'rows': 'pc64', 'cols': 'pc128'}[c]
-        rec['kernel_us_source'] = f'profiles/{a.tag}/{cfg}_kernel_stats.csv (AverageNs)'
+        rec['kernel_us_source'] = (f'profiles/{a.tag}/{cfg}_kernel_trace.csv (median over the dispatches; '
+                                   f'the --stats average is kernel_us_rocprof_avg, {cfg}_kernel_stats.csv)')
         rec['counter_source'] = f'profiles/{a.tag}/{cfg}_counters.csv'
     bench = trace_stats(os.path.join(a.dir, 'bench_trace'))
     if bench:
