@@ -41,19 +41,33 @@ class _PinnedArrays:
     one per ``.posecells`` read: the GPU writes the volume straight into the array
     the caller gets (rs_pc_read_pinned), so the readback needs no host-side copy.
     Each array owns its block until it is garbage-collected, when the block goes
-    back to the free list (the caller's arrays never alias one another)."""
+    back to the free list (the caller's arrays never alias one another).  At most
+    ``cap`` blocks exist at once: a caller that keeps every volume (a history list)
+    gets ordinary pageable arrays past that (``array`` returns None), so pinned host
+    memory stays bounded."""
 
-    def __init__(self, lib, n):
-        self._lib, self._n = lib, n
+    CAP = 8
+
+    def __init__(self, lib, n, cap=CAP):
+        self._lib, self._n, self._cap = lib, n, cap
         self._free = []
+        self._blocks = 0
         self._lock = threading.Lock()
 
     def array(self, shape):
         with self._lock:
             ptr = self._free.pop() if self._free else None
+            if ptr is None:
+                if self._blocks >= self._cap:
+                    return None, None
+                self._blocks += 1
         if ptr is None:
             p = ctypes.c_void_p()
-            _lib.check(self._lib.rs_host_alloc(8 * self._n, ctypes.byref(p)))
+            st = self._lib.rs_host_alloc(8 * self._n, ctypes.byref(p))
+            if st != _lib.RS_OK:
+                with self._lock:
+                    self._blocks -= 1
+                _lib.check(st)
             ptr = p.value
         view = (ctypes.c_double * self._n).from_address(ptr)
         weakref.finalize(view, self._release, ptr).atexit = False  # the process frees it at exit
@@ -181,7 +195,11 @@ class PoseCellNetwork:
                 out, self._fresh = self._fresh, None
                 return out
             out, ptr = self._pinned_array()
-            _lib.check(self._lib.rs_pc_read_pinned(self._h, ctypes.c_void_p(ptr)))
+            if out is None:   # the pinned pool is all held by the caller: pageable copy
+                out = np.empty(self.shape, dtype=np.float64)
+                _lib.check(self._lib.rs_pc_read(self._h, _lib.ptr(out, ctypes.c_double)))
+            else:
+                _lib.check(self._lib.rs_pc_read_pinned(self._h, ctypes.c_void_p(ptr)))
         return out
 
     def _pinned_array(self):
@@ -241,8 +259,8 @@ class PoseCellNetwork:
         out = self._out3
         with self._mutex:
             self._fresh = None
-            if self._eager:
-                arr, ptr = self._pinned_array()
+            arr, ptr = self._pinned_array() if self._eager else (None, None)
+            if arr is not None:
                 st = self._update_odom_read(self._h, vtrans, vrot, self._out3_addr, ptr)
                 if st == _lib.RS_OK:
                     self._fresh = arr

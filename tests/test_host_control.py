@@ -177,3 +177,49 @@ def test_library_control_bit_identical_to_numpy(th):
         assert np.array_equal(rows[i], rr), (i, vt, vr)
         assert zf[i].tobytes() == zz.tobytes(), (i, vt, vr)
     assert n_ok > 5000 and n_key > 100 and n_range > 0
+
+
+def test_pinned_pool_reuses_and_caps_blocks():
+    """_PinnedArrays (the .posecells readback pool) with a host stand-in for
+    rs_host_alloc: freed arrays' blocks are reused, at most CAP exist at once (then
+    array() returns None and the caller copies into pageable memory), and close()
+    frees the free list and later releases."""
+    import ctypes
+    import gc
+    from pyratslam_amd import _lib
+    from pyratslam_amd.posecell_network import _PinnedArrays
+
+    class FakeLib:
+        def __init__(self):
+            self.live = {}
+
+        def rs_host_alloc(self, nbytes, out):
+            buf = ctypes.create_string_buffer(nbytes)
+            out._obj.value = ctypes.addressof(buf)
+            self.live[ctypes.addressof(buf)] = buf
+            return _lib.RS_OK
+
+        def rs_host_free(self, ptr):
+            del self.live[ptr.value]
+            return _lib.RS_OK
+
+    lib = FakeLib()
+    pool = _PinnedArrays(lib, 6, cap=3)
+    a, pa = pool.array((2, 3))
+    b, pb = pool.array((2, 3))
+    assert a.shape == (2, 3) and pa != pb and len(lib.live) == 2
+    a[:] = 1.0
+    del a
+    gc.collect()
+    c, pc = pool.array((2, 3))
+    assert pc == pa and len(lib.live) == 2        # reused, not a new block
+    d, pd = pool.array((2, 3))
+    e, pe = pool.array((2, 3))
+    assert d is not None and e is None and pe is None and pool._blocks == 3
+    del c
+    gc.collect()
+    pool.close()
+    assert len(lib.live) == 2                     # the free block went at close
+    del b, d
+    gc.collect()
+    assert lib.live == {}                         # released after close: freed

@@ -432,6 +432,35 @@ def test_posecells_pinned_readback_arrays_are_independent(pcn, precision):
             assert np.array_equal(a, snap)
 
 
+@pytest.mark.parametrize('readback', ['lazy', 'eager'])
+def test_posecells_kept_history_bounds_pinned_pool(pcn, readback):
+    """A caller that keeps every volume (a history list) holds the pinned pool's
+    blocks; past _PinnedArrays.CAP reads fall back to pageable copies and stay
+    correct, and pinned host memory stays bounded."""
+    from pyratslam_amd.posecell_network import _PinnedArrays
+    shape = (32, 32, 18)
+    net = pcn(shape, readback=readback)
+    ref = P.PoseCellOracle(shape)
+    net.inject(1, (16, 16, 9))
+    ref.inject(1, (16, 16, 9))
+    hist, want = [], []
+    for v in odometry(3 * _PinnedArrays.CAP, 11):
+        net.update(v)
+        ref.update(v)
+        hist.append(net.posecells)
+        want.append(ref.posecells.copy())
+    assert net._pinned._blocks <= _PinnedArrays.CAP
+    for a, b in zip(hist, want):
+        assert np.abs(a - b).max() < F32_TOL
+    assert len({a.ctypes.data for a in hist}) == len(hist)
+    del hist
+    v = odometry(1, 12)[0]
+    net.update(v)
+    ref.update(v)
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+    net.close()
+
+
 def test_eager_readback_equals_lazy(pcn):
     """readback='eager': update() exports the new volume before its one sync and the
     next .posecells returns it; identical to the lazy readback after every update,
