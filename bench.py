@@ -490,15 +490,21 @@ def cpu_baseline(args):
     # short sample; the faster one runs the baseline (a mask wider than the job's
     # CPU quota oversubscribes it)
     cands = sorted({c for c in (C.threads(), host['affinity_cpus'] or 0) if c > 0})
+    # (4 queries per call: the oracle parallelises each query over the templates, and
+    # an oversubscribed mask runs a few queries per second, so a larger call would
+    # hold the probe for many seconds past its time limit)
     probe = {}
     for c in cands:
         C.set_threads(c)
-        C.vt_best(lib, qs[:64])                      # thread pool up
+        span = min(1.0, budget / 4)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < span:       # thread pool up (its first calls run slow)
+            C.vt_best(lib, qs[:4])
         n = 0
         t0 = time.perf_counter()
-        while time.perf_counter() - t0 < min(1.0, budget / 4):
-            C.vt_best(lib, qs[n % 4096:n % 4096 + 64])
-            n += 64
+        while time.perf_counter() - t0 < span:
+            C.vt_best(lib, qs[n % 4096:n % 4096 + 4])
+            n += 4
         probe[c] = n / (time.perf_counter() - t0)
     best = max(probe, key=probe.get)
     C.set_threads(best)
