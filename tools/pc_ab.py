@@ -2,6 +2,7 @@
 """A/B timing of the pose-cell step across library builds (GPU box).
 
 usage: python tools/pc_ab.py LIB.so[@ENV=V,...] [LIB2.so ...] [--shape 128,128,72] [--steps 2000] [--rounds 3]
+       [--mode run|update|node]
 (``@RS_PC_CTL=inline`` runs that library with the variable set)
 Each library runs in its own process (ctypes loads one copy), interleaved over
 rounds so clock drift hits every build alike: batched run() steps/s after a clock
@@ -17,15 +18,33 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(path, shape, steps, check, precision, out):
+def child(path, shape, steps, check, precision, out, mode='run'):
     sys.path.insert(0, ROOT)
     import numpy as np
     from pyratslam_amd import _lib, synthetic
     _lib.load(path)
     from pyratslam_amd import PoseCellNetwork
     od = synthetic.odometry(steps + check + 50, seed=0)
-    net = PoseCellNetwork(shape, precision=precision)
+    net = PoseCellNetwork(shape, precision=precision, readback='eager' if mode == 'node' else 'lazy')
     net.inject(1, tuple(s // 2 for s in shape))
+    if mode != 'run':  # per-call update() ('update'), or update() + .posecells ('node')
+        def one(v):
+            net.update(v)
+            if mode == 'node':
+                net.posecells
+        for v in od[:check]:
+            one(v)
+        np.save(out, net.posecells)   # the state every build reaches on the same odometry
+        t_end = time.perf_counter() + 0.3
+        while time.perf_counter() < t_end:
+            for v in od[check:check + 50]:
+                one(v)
+        t0 = time.perf_counter()
+        for v in od[check + 50:check + 50 + steps]:
+            one(v)
+        dt = time.perf_counter() - t0
+        print(json.dumps({'lib': path, 'mode': mode, 'us_per_step': 1e6 * dt / steps, 'argmax': []}), flush=True)
+        return
     mx = net.run(od[:check])
     np.save(out, net.posecells)
     t_end = time.perf_counter() + 0.3          # clock warm-up
@@ -48,10 +67,12 @@ def main():
     ap.add_argument('--precision', default='float32')
     ap.add_argument('--child', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--out', default='')
+    ap.add_argument('--mode', default='run', choices=('run', 'update', 'node'),
+                    help="batched run() (default), per-call update(), or update() + .posecells (eager)")
     a = ap.parse_args()
     shape = tuple(int(s) for s in a.shape.split(','))
     if a.child:
-        child(a.libs[0], shape, a.steps, a.check, a.precision, a.out)
+        child(a.libs[0], shape, a.steps, a.check, a.precision, a.out, a.mode)
         return
     import numpy as np
     res = {lib: [] for lib in a.libs}
@@ -62,7 +83,7 @@ def main():
             env = dict(os.environ, **dict(kv.split('=', 1) for kv in envs.split(',') if kv))
             p = subprocess.run([sys.executable, __file__, path, '--child', '--shape', a.shape, '--steps',
                                 str(a.steps), '--check', str(a.check), '--precision', a.precision,
-                                '--out', out], capture_output=True, text=True, timeout=300, env=env)
+                                '--out', out, '--mode', a.mode], capture_output=True, text=True, timeout=300, env=env)
             if p.returncode != 0:
                 print(p.stderr[-3000:], file=sys.stderr)
                 raise SystemExit(p.returncode)
