@@ -170,14 +170,18 @@ int rs_pc_total(rs_pc* h, double* total);
  * the step's launches; recorded only while profiling is enabled, else 0 -- the two
  * event records cost about 1.5 us of a 31 us update() call) */
 int rs_pc_last_ms(rs_pc* h, double* ms);
-/* HIP-event time of each kernel of the last rs_pc_run, summed over its steps:
- * ms[0] = excitation kernel, ms[1] = path-integration kernel (events recorded
- * around every launch on the handle's stream; only when profiling is enabled) */
+/* profiling: enable = 1 records HIP events around the whole call (rs_pc_last_ms)
+ * and around every launch (rs_pc_kernel_ms; the per-launch events add gaps between
+ * the kernels); enable = 2 only around the whole call; 0 none.
+ * rs_pc_kernel_ms: the event time of each kernel of the last rs_pc_run, summed over its
+ * steps: ms[0] = the step kernel (excitation kernel of the two-launch forms, the one
+ * kernel of the halo form), ms[1] = path-integration kernel (halo form: pc_halo_finish) */
 int rs_pc_set_profiling(rs_pc* h, int enable);
 int rs_pc_kernel_ms(rs_pc* h, double ms[2]);
 /* step kernels in use: "rows" (row-tiled excite + path launches, Y <= 128),
- * "cols" (column tiles through all layers, large grids), "stream" (layer
- * streaming, large grids outside the column form's limits) or "tiles" (3-D tiles) */
+ * "cols" (column tiles through all layers, large grids), "halo" (one launch per
+ * step, the excitation recomputed on each tile's halo; float32, TH = 36), "stream"
+ * (layer streaming, large grids outside the column form's limits) or "tiles" (3-D tiles) */
 const char* rs_pc_step_form(const rs_pc* h);
 /* Test hooks (no reference counterpart):
  *   RS_PC_DBG_POISON       fill every buffer a step writes before it reads (the

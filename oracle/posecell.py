@@ -126,9 +126,10 @@ def step_control(vtrans, vrot, shape, lut, lut_precision=10):
     vr = vrot / vrot_scale
     mid = th // 2
     ang = (np.arange(th).reshape((1, th)) - mid) * vrot_scale
-    exact = np.concatenate((vt * np.cos(ang), vt * np.sin(ang)), axis=0)
-    rounded = np.concatenate((np.around(vt * np.cos(ang)), np.around(vt * np.sin(ang))), axis=0)
-    resid = exact - rounded
+    with np.errstate(invalid='ignore', over='ignore'):   # non-finite vtrans: NaN residuals, as numpy gives
+        exact = np.concatenate((vt * np.cos(ang), vt * np.sin(ang)), axis=0)
+        rounded = np.concatenate((np.around(vt * np.cos(ang)), np.around(vt * np.sin(ang))), axis=0)
+        resid = exact - rounded
     keys = []
     filters = np.empty((7, 7, th))
     for z in range(th):
@@ -138,7 +139,10 @@ def step_control(vtrans, vrot, shape, lut, lut_precision=10):
             filters[:, :, z] = lut[(k, k)]
         except KeyError as e:
             raise LutKeyError((k, k)) from e
-    z_origin = math.floor(vr + .5)
+    # Python 2: math.floor returns a NaN / infinite argument unchanged, and the 1-D
+    # filter built on it is all NaN (exp(NaN), or 0/0 in its normalisation) -- the
+    # reference runs on with a NaN volume; Python 3's floor would raise instead
+    z_origin = math.floor(vr + .5) if math.isfinite(vr + .5) else vr + .5
     return {
         'ox': rounded[0].astype(np.int32),
         'oy': rounded[1].astype(np.int32),
@@ -146,7 +150,7 @@ def step_control(vtrans, vrot, shape, lut, lut_precision=10):
         'filters': filters,
         'radius': int(np.ceil(abs(vt))),
         'z_origin': z_origin,
-        'zf': dog_offset_1d(z_origin),
+        'zf': dog_offset_1d(z_origin) if math.isfinite(z_origin) else np.full(7, np.nan),
     }
 
 

@@ -27,6 +27,8 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
+#include <limits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -48,6 +50,52 @@ struct SepKernel {
     T gi[FL];
     T scale;
     T inhib;
+};
+
+// The normalisation P /= total (posecell_network.py:343-345).  float32: a product with
+// the reciprocal of the total, rounded once from double (within an ulp of the division;
+// one VALU op per value); where that reciprocal is not a finite float (a total below
+// about 2.9e-39) each value is divided instead.  float64: the division, as the reference.
+// A zero total leaves the volume as it is (:344).
+template <typename T>
+struct PcNorm;
+template <>
+struct PcNorm<float> {
+    float r, t;
+    bool div;
+    __device__ explicit PcNorm(double tot) {
+        const float rf = (float)(tot != 0.0 ? 1.0 / tot : 1.0);
+        // wave-uniform (every lane formed the same total): a scalar branch below, so the
+        // division is never speculated into the common path
+        div = __builtin_amdgcn_readfirstlane((int)!__builtin_isfinite(rf)) != 0;
+        r = div ? 1.0f : rf;
+        t = div ? (float)tot : 1.0f;
+    }
+    __device__ float operator()(float x) const {
+        float y = x * r;
+        if (div) {
+            asm volatile("" ::: "memory");
+            y = x / t;
+        }
+        return y;
+    }
+    template <int N>
+    __device__ void operator()(float (&p)[N]) const {
+        if (div) {
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < N; ++q) p[q] = p[q] / t;
+        } else {
+#pragma unroll
+            for (int q = 0; q < N; ++q) p[q] = p[q] * r;
+        }
+    }
+};
+template <>
+struct PcNorm<double> {
+    double t;
+    __device__ explicit PcNorm(double tot) : t(tot != 0.0 ? tot : 1.0) {}
+    __device__ double operator()(double x) const { return x / t; }
 };
 
 // Per-step control of the path-integration kernel: inline by value (one launch
@@ -92,8 +140,19 @@ constexpr int RES_SLOTS = 256;
 // RES_NONE into each step's result word before the launch and refuses a result
 // still holding it after the stream has synchronised.
 constexpr unsigned long long RES_NONE = 0ull;
+// Step outputs are >= 0 or NaN (every step ends in a clamp), so the value bits order
+// like the values; every NaN is given one bit pattern above +inf, so that, as in numpy's
+// argmax, a NaN beats every number and the first NaN wins.
 __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
-    return ((unsigned long long)__float_as_uint(v) << 32) | (0xFFFFFFFFu - lin);
+    const unsigned bits = v != v ? 0x7FC00000u : __float_as_uint(v);
+    return ((unsigned long long)bits << 32) | (0xFFFFFFFFu - lin);
+}
+// The same order for (value, index) pairs (float64 steps, get_pc_max): a NaN beats every
+// number, ties and NaNs among themselves go to the lower index; start from (-inf, ~0u).
+template <typename T>
+__device__ inline bool pc_better(T v, unsigned l, T bv, unsigned bl) {
+    const bool vn = v != v, bn = bv != bv;
+    return vn ? (!bn || l < bl) : (!bn && (v > bv || (v == bv && l < bl)));
 }
 
 // Phase-stamp hooks, empty in the library.  tools/pc_probe.hip defines them (a
@@ -292,9 +351,9 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
     __syncthreads();
 
     // theta filter, clamp (:310-314), normalise, store, argmax
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
-    const T tt = (T)tot;
+    const PcNorm<T> nrm(tot);
     for (int idx = tid; idx < BK * BX * BY; idx += NT) {
         const int kq = idx / (BX * BY);
         const int rem = idx - kq * (BX * BY);
@@ -305,10 +364,10 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
 #pragma unroll
             for (int z = 0; z < FL; ++z) acc += s_r[idx + z * BX * BY] * s_zf[z];
             T v = acc > T(0) ? acc : T(0);
-            if (tot != 0.0) v = v / tt;
+            v = nrm(v);
             P[((size_t)gk * X + gi) * Y + gj] = v;
             const unsigned lin = ((unsigned)gi * Y + gj) * TH + gk;
-            if (v > bv || (v == bv && lin < bl)) {
+            if (pc_better(v, lin, bv, bl)) {
                 bv = v;
                 bl = lin;
             }
@@ -321,7 +380,7 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
         for (int off = 32; off > 0; off >>= 1) {
             const T ov = __shfl_xor(bv, off);
             const unsigned ol = __shfl_xor(bl, off);
-            if (ov > bv || (ov == bv && ol < bl)) {
+            if (pc_better(ov, ol, bv, bl)) {
                 bv = ov;
                 bl = ol;
             }
@@ -333,7 +392,7 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
         __syncthreads();
         if (tid == 0) {
             for (int w = 1; w < NT / 64; ++w)
-                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                if (pc_better(s_bv[w], s_bl[w], bv, bl)) {
                     bv = s_bv[w];
                     bl = s_bl[w];
                 }
@@ -668,11 +727,11 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 
     // theta filter (:310), clamp (:314), normalise (:343-345), store, argmax (:317-319):
     // float32 as the largest packed (value, ~index) key, float64 as value/index pairs
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
     {
-        const T tt = tot != 0.0 ? T(1) / (T)tot : T(1);  // as the column form
+        const PcNorm<T> nrm(tot);
         const int kq = wave / BX, i = wave - kq * BX;
         const int gk = k0 + kq, gi = i0 + i;
         if (gk < TH && gi < X) {
@@ -684,12 +743,12 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
 #pragma unroll
                 for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * (T)ctl_zf(ctl, z);
                 T val = acc > T(0) ? acc : T(0);
-                val = val * tt;
+                val = nrm(val);
                 st_wt(&P[((size_t)gk * X + gi) * Y + j], val);
                 const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
                 if constexpr (sizeof(T) == 4) {
                     bk = max(bk, argmax_key((float)val, lin));
-                } else if (val > bv || (val == bv && lin < bl)) {
+                } else if (pc_better(val, lin, bv, bl)) {
                     bv = val;
                     bl = lin;
                 }
@@ -712,7 +771,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
         for (int off = 32; off > 0; off >>= 1) {
             const T ov = __shfl_xor(bv, off);
             const unsigned ol = __shfl_xor(bl, off);
-            if (ov > bv || (ov == bv && ol < bl)) {
+            if (pc_better(ov, ol, bv, bl)) {
                 bv = ov;
                 bl = ol;
             }
@@ -724,7 +783,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
         co_lds_barrier();
         if (tid == 0) {
             for (int w = 1; w < NW; ++w)
-                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                if (pc_better(s_bv[w], s_bl[w], bv, bl)) {
                     bv = s_bv[w];
                     bl = s_bl[w];
                 }
@@ -1040,10 +1099,10 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #pragma unroll
     for (int u = 0; u < NPP; ++u) tot += tid + u * NT < npart ? pt[u] : 0.0;
     tot = block_sum_w<NW>(tot, s_red);
-    const T tt = (T)tot;
+    const PcNorm<T> nrm(tot);
 
     T ring[FL][BX];
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     // software-pipelined: iteration it stores window it+1 while filtering window it;
     // one barrier per iteration
@@ -1093,11 +1152,11 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
 #pragma unroll
                     for (int z = 0; z < FL; ++z) v += ring[(s + 1 + z) % FL][i] * zf[z];
                     v = v > T(0) ? v : T(0);
-                    if (tot != 0.0) v = v / tt;
+                    v = nrm(v);
                     s_out[(o * BXB + rg * BX + i) * YT + col] = v;
                     const int gi = i0 + rg * BX + i;
                     const unsigned lin = ((unsigned)gi * Y + gy) * TH + gk;
-                    if (gi < X && gy < Y && (v > bv || (v == bv && lin < bl))) {
+                    if (gi < X && gy < Y && pc_better(v, lin, bv, bl)) {
                         bv = v;
                         bl = lin;
                     }
@@ -1119,7 +1178,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     for (int off = 32; off > 0; off >>= 1) {
         const T ov = __shfl_xor(bv, off);
         const unsigned ol = __shfl_xor(bl, off);
-        if (ov > bv || (ov == bv && ol < bl)) {
+        if (pc_better(ov, ol, bv, bl)) {
             bv = ov;
             bl = ol;
         }
@@ -1131,7 +1190,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
     __syncthreads();
     if (tid == 0) {
         for (int w = 1; w < NW; ++w)
-            if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+            if (pc_better(s_bv[w], s_bl[w], bv, bl)) {
                 bv = s_bv[w];
                 bl = s_bl[w];
             }
@@ -1620,10 +1679,8 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
     for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
     tot = co_wave_sum(tot);
-    // the normalisation (:343-345) as a product with the reciprocal (one VALU op per
-    // output instead of a correctly rounded division; within an ulp of it); a zero
-    // total leaves the volume as it is, as the reference does
-    const T tt = tot != 0.0 ? T(1) / (T)tot : T(1);
+    // the normalisation (:343-345): PcNorm (float32: the product with the reciprocal)
+    const PcNorm<T> nrm(tot);
 #pragma unroll
     for (int u = 0; u < NFR; ++u) {
         const int i = tid + u * NT, fi = i / FT;
@@ -1812,7 +1869,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // theta pass, clamp, normalisation, argmax: task (cell p, chunk j).  float32:
     // the first maximum as the largest packed (value, ~index) key; float64: value
     // and index pairs
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     unsigned long long bk = 0ull;
     {
@@ -1847,7 +1904,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 #pragma unroll
                 for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
                 x = x > T(0) ? x : T(0);
-                x = x * tt;
+                x = nrm(x);
                 v[o] = x;
             }
             if (gi < X && gy < Y) {
@@ -1866,7 +1923,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                     const unsigned lin = (unsigned)(e0 + o);
                     if constexpr (sizeof(T) == 4) {
                         bk = max(bk, argmax_key((float)v[o], lin));
-                    } else if (v[o] > bv || (v[o] == bv && lin < bl)) {
+                    } else if (pc_better(v[o], lin, bv, bl)) {
                         bv = v[o];
                         bl = lin;
                     }
@@ -1888,7 +1945,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         for (int off = 32; off > 0; off >>= 1) {
             const T ov = __shfl_xor(bv, off);
             const unsigned ol = __shfl_xor(bl, off);
-            if (ov > bv || (ov == bv && ol < bl)) {
+            if (pc_better(ov, ol, bv, bl)) {
                 bv = ov;
                 bl = ol;
             }
@@ -1900,7 +1957,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         co_lds_barrier();
         if (tid == 0) {
             for (int w = 1; w < NW; ++w)
-                if (s_bv[w] > bv || (s_bv[w] == bv && s_bl[w] < bl)) {
+                if (pc_better(s_bv[w], s_bl[w], bv, bl)) {
                     bv = s_bv[w];
                     bl = s_bl[w];
                 }
@@ -1909,6 +1966,457 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         }
     }
     PC_STAMP(6, 4);
+}
+
+// ---------------------------------------------------------------------------
+// Halo form: ONE launch per step (float32; X, Y >= HF_W; TH == HF_TH).
+//
+// The reference's step (posecell_network.py:326-353) has one global dependency, the
+// normalisation total (:343-345), and two local ones: the excitation's 3-cell halo
+// (:336) and the path filter's shifted 7 x 7 window (:273).  The two-launch forms
+// hand the excited volume Q from one kernel to the next through memory.  Here a
+// block recomputes the excitation on its halo instead, so the only hand-off left is
+// the one a kernel boundary gives for free: the state and its total.
+//  * Between the launches of a batch the state is kept UNNORMALISED,
+//    U = relu(conv_z(relu(conv_xy(Q)))), with the per-block partial sums of the
+//    total t of Q (max(conv(Q/t), 0) = max(conv(Q), 0)/t for t > 0, which the
+//    two-launch forms use too).  The next launch sums the partials and forms
+//    P = U * (1/t) as it loads: the same product
+//    the two-launch path kernels apply before their store, so P is the same.
+//  * The argmax of a step (:317-319) is taken from those scaled values, exactly the
+//    values of the state: by the next launch over its own tile, and for the last step
+//    of a call by pc_halo_finish, which also stores the normalised state (between
+//    calls the handle's state is normalised, as in every other form) and exports the
+//    keys of all steps to the host (its last block, by an agent-scope counter).
+//  * A block owns a 4 x 4 tile through all TH layers (256 blocks at 64 x 64).  Layer
+//    j's path output needs Q on the 10 x 10 window shifted by the layer's (ox, oy),
+//    and that Q needs P on the 16 x 16 window around it.  The excitation runs theta
+//    pass first: the union of the step's shifted 16 x 16 windows goes global -> LDS
+//    by LDS-DMA (each cell's theta column is contiguous, theta-fastest C order, so the
+//    pieces are whole 1 KiB runs per wave-instruction), a thread then takes one
+//    cell's column, scales it, forms all TH theta-pass outputs in registers and
+//    stores those of the windows that hold the cell; then per layer on its own
+//    window the y pass (16 x 10), the x pass (10 x 10) with the inhibition, the 7 x 7
+//    path filter and clamp, the theta filter and clamp, and the write-through store.
+//  * The partial sums cover, for layer j, the block's tile shifted by layer j's
+//    shift (the centre of its Q window): those shifted tiles partition each layer as
+//    the tiles do.
+// ---------------------------------------------------------------------------
+constexpr int HF_T = 4;                       // tile: HF_T x HF_T cells through all layers
+constexpr int HF_W = HF_T + 4 * HALF;         // 16: a layer's excitation window
+constexpr int HF_Q = HF_T + 2 * HALF;         // 10: a layer's excited (Q) window
+constexpr int HF_NW = 9, HF_NT = 64 * HF_NW;  // 576 threads: one task per (layer, window row) at TH = 36
+constexpr int HF_TH = 36;                     // the theta extent instantiated (configs[1], the ROS node)
+constexpr int HF_UMAX = 22 * 22;              // union cells staged by LDS-DMA (|shifts| spread <= 6)
+constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;  // theta-pass window rows: pitch 18 (the y pass's 8-byte row reads are conflict-free)
+constexpr int HF_YJ = HF_W * HF_Q + 10;       // y-pass outputs per layer (pitch: the x pass reads conflict-free)
+constexpr int HF_QJ = HF_Q * HF_Q + 4;        // Q window per layer
+constexpr int HF_EXP_MAX = 64;                // steps whose keys pc_halo_finish exports itself
+
+// One step's control, a kernel argument (formed on the host by make_ctl_halo).
+struct PcCtlHalo {
+    short sx[HF_TH], sy[HF_TH];  // layer j's 16 x 16 window starts at union row sx[j], column sy[j]
+    unsigned char fo[HF_TH];     // layer j's path filter (row of the filter table)
+    float zf[FL];                // theta filter (posecell_network.py:308)
+    short ux, uy;                // union origin = tile origin - 6 + the smallest centred shift
+    short uw, uh;                // union extent in cells (at most X, Y)
+    int wrap;                    // the union is a whole period in x or y (windows wrap inside it)
+};
+typedef float hf_f2 __attribute__((ext_vector_type(2)));  // (excitatory, inhibitory) pairs: packed FMAs
+
+// The normalisation total of a step from its per-block partials, formed by every wave
+// itself in one fixed order (so every block gets the same bits): 4 per lane, then DPP.
+__device__ inline double pc_partials_total(const double* __restrict__ part, int npart) {
+    const int lane = threadIdx.x & 63, np1 = npart > 0 ? npart - 1 : 0;
+    double pt[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pt[u] = part[min(lane + 64 * u, np1)];  // unconditional
+    double tot = 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
+    for (int i = lane + 256; i < npart; i += 64) tot += part[i];
+    return co_wave_sum(tot);
+}
+
+// EXC: excitation only (rs_pc_excite, the step the reference runs before a LUT
+// KeyError): zero shifts, Q of the own cells stored into Uo (theta-fastest), partials.
+template <bool EXC>
+__global__ __launch_bounds__(HF_NT) void pc_step_halo(
+    const float* __restrict__ U, float* __restrict__ Uo, const double* __restrict__ part_in,
+    int npart_in, double* __restrict__ part_out, unsigned long long* __restrict__ slot_prev,
+    unsigned long long* __restrict__ slot_zero, const float* __restrict__ filt, int nf, PcCtlHalo ctl,
+    int X, int Y, int gx, SepKernel<float> k) {
+    constexpr int TH = HF_TH, NV = TH / 4;   // 16-byte pieces per theta column
+    static_assert(TH % 4 == 0, "theta columns of whole 16-byte pieces");
+    constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
+    constexpr int YBUF = 2 * TH * HF_YJ;
+    constexpr int BBUF = WBUF > YBUF ? WBUF : YBUF;
+    constexpr int PP = TH + 64;   // path outputs per cell: rows TH dwords apart modulo the 64 banks
+    static_assert(HF_T * HF_T * PP <= BBUF && TH * HF_QJ <= 2 * TH * HF_WJ, "buffer reuse");
+    __shared__ __attribute__((aligned(16))) float s_t[2 * TH * HF_WJ];  // theta pass e | i; then Q
+    __shared__ __attribute__((aligned(16))) float s_b[BBUF];  // union image; then y pass e | i; then path outputs
+    __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
+    __shared__ int s_fo[TH];
+    __shared__ double s_red[HF_NW];
+    __shared__ unsigned long long s_bk[HF_NW];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int x0 = (tile % gx) * HF_T, y0 = (tile / gx) * HF_T;
+    const int tw = min(HF_T, X - x0), tht = min(HF_T, Y - y0);
+    const int UW = ctl.uw, UH = ctl.uh, nu = UW * UH;
+    const int ux0 = co_wrap(x0 - 2 * HALF + ctl.ux, X), uy0 = co_wrap(y0 - 2 * HALF + ctl.uy, Y);
+    const bool dma = nu <= HF_UMAX;
+    PC_STAMP(7, 0);
+    // 1. the union image, issued first: piece p = tid + HF_NT * r is 16-byte piece p % NV
+    //    of union cell p / NV (cells row-major, UH per row), landing at s_b + 4p
+    if (dma) {
+        constexpr int DC = HF_NT / NV, DL = HF_NT % NV, NR = (HF_UMAX * NV + HF_NT - 1) / HF_NT;
+        const int npc = nu * NV, dU = DC / UH, dV = DC - dU * UH;
+        int c = tid / NV, l4 = tid - c * NV, ui = c / UH, vi = c - ui * UH;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int i0 = r * HF_NT + wave * 64;  // wave-uniform
+            if (i0 < npc) {
+                if (i0 + lane < npc) {
+                    int gr = ux0 + ui, gc = uy0 + vi;
+                    gr -= gr >= X ? X : 0;
+                    gc -= gc >= Y ? Y : 0;
+                    __builtin_amdgcn_global_load_lds(
+                        (__attribute__((address_space(1))) const void*)(U + ((unsigned)gr * Y + gc) * TH + 4 * l4),
+                        (__attribute__((address_space(3))) void*)(s_b + 4 * i0), 16, 0, 0);
+                }
+            }
+            l4 += DL;
+            vi += dV;
+            ui += dU;
+            if (l4 >= NV) {
+                l4 -= NV;
+                ++vi;
+            }
+            if (vi >= UH) {
+                vi -= UH;
+                ++ui;
+            }
+        }
+    }
+    // the normalisation of the state entering the step, the filter table, the control
+    const float fr = tid < nf * FT ? filt[tid] : 0.f;
+    static_assert(RT_NFMAX * FT <= HF_NT, "one filter tap per thread");
+    if (tid < TH) s_fo[tid] = ctl.fo[tid] * ST_FTP;
+    const PcNorm<float> nrm(pc_partials_total(part_in, npart_in));
+    if (tid < nf * FT) s_ftab[(tid / FT) * ST_FTP + tid % FT] = fr;
+    if (slot_zero != nullptr && blockIdx.x == 0)
+        for (int i = tid; i < RES_SLOTS; i += HF_NT) st_wt(&slot_zero[i], 0ull);  // the next launch max-reduces into them
+    if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces have landed
+    co_lds_barrier();
+    PC_STAMP(7, 1);
+
+    // 2. per union cell: its column, scaled (the argmax of the state entering the step,
+    //    own tile), the theta pass of both Gaussians as packed (e, i) FMAs, stored for
+    //    every layer window holding the cell.  Windows are [j][rx][ry] with row pitch
+    //    HF_WP, so a cell's place in layer j's window, j*HF_WJ + (ui-sx_j)*HF_WP + vi-sy_j,
+    //    is the cell's own offset plus a per-layer scalar (no per-layer address math);
+    //    only a union spanning a whole period (wrap) needs the modular form.
+    float* s_te = s_t;
+    float* s_ti = s_t + TH * HF_WJ;
+    unsigned long long bk = 0ull;
+    const bool want_key = slot_prev != nullptr;
+    hf_f2 gei[FL];
+#pragma unroll
+    for (int t = 0; t < FL; ++t) gei[t] = hf_f2{k.ge[t], k.gi[t]};
+    // one union cell c: FAST = the column from the LDS-DMA image and no wrap (the
+    // common case: straight-line code, one cell per thread); otherwise the column from
+    // memory or the windows wrapping inside a whole-period union
+    auto cell_pass = [&](int c, auto fast_c, auto wrap_c) __attribute__((always_inline)) {
+        constexpr bool FAST = decltype(fast_c)::value, WRAP = decltype(wrap_c)::value;
+        const int ui = c / UH, vi = c - ui * UH;
+        int gr = ux0 + ui, gc = uy0 + vi;
+        gr -= gr >= X ? X : 0;
+        gc -= gc >= Y ? Y : 0;
+        float p[TH];
+        const co_f4* src = FAST || dma ? reinterpret_cast<const co_f4*>(s_b + c * TH)
+                                       : reinterpret_cast<const co_f4*>(U + ((size_t)gr * Y + gc) * TH);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const co_f4 x = src[v];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
+        }
+        nrm(p);
+        if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
+            const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
+#pragma unroll
+            for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
+        }
+        // the cell's own offset, opaque to the compiler: each layer's window place is
+        // then one add of a scalar, not a re-derived product
+        int cb = ui * HF_WP + vi;
+        asm volatile("" : "+v"(cb));
+#pragma unroll
+        for (int j = 0; j < TH; ++j) {
+            const int sxj = ctl.sx[j], syj = ctl.sy[j];
+            int a;
+            bool in;
+            if constexpr (WRAP) {
+                int rx = ui - sxj, ry = vi - syj;
+                rx += rx < 0 ? UW : 0;
+                ry += ry < 0 ? UH : 0;
+                in = (unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W;
+                a = j * HF_WJ + rx * HF_WP + ry;
+            } else {
+                in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
+                a = cb + __builtin_amdgcn_readfirstlane(j * HF_WJ - sxj * HF_WP - syj);
+            }
+            if (in) {
+                hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < FL; ++t) eg += gei[t] * p[(j + t + TH - HALF) % TH];
+                s_te[a] = eg.x;
+                s_ti[a] = eg.y;
+            }
+        }
+    };
+    if (dma && !ctl.wrap) {
+        if (tid < nu) cell_pass(tid, std::true_type{}, std::false_type{});
+    } else if (ctl.wrap) {
+#pragma unroll 1
+        for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{}, std::true_type{});
+    } else {
+#pragma unroll 1
+        for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{}, std::false_type{});
+    }
+    if (want_key && tid < tw * tht) {
+        // an own cell outside the union (a large uniform shift): its key from memory
+        const int i = tid / tht, j = tid - i * tht;
+        int cu = co_wrap(2 * HALF - ctl.ux, X) + i, cv = co_wrap(2 * HALF - ctl.uy, Y) + j;
+        cu -= cu >= X ? X : 0;
+        cv -= cv >= Y ? Y : 0;
+        if (cu >= UW || cv >= UH) {
+            const unsigned lin0 = ((unsigned)(x0 + i) * Y + (y0 + j)) * TH;
+            const co_f4* src = reinterpret_cast<const co_f4*>(U + lin0);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const co_f4 x = src[v];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) bk = max(bk, argmax_key(nrm(x[w]), lin0 + 4 * v + w));
+            }
+        }
+    }
+    co_lds_barrier();
+    PC_STAMP(7, 2);
+
+    // 3. y pass: task (layer j, window row rx) -> 10 outputs of each Gaussian
+    float* s_ye = s_b;
+    float* s_yi = s_b + TH * HF_YJ;
+    for (int t = tid; t < TH * HF_W; t += HF_NT) {
+        const int j = t >> 4, rx = t & 15;
+        const hf_f2* re = reinterpret_cast<const hf_f2*>(s_te + j * HF_WJ + rx * HF_WP);
+        const hf_f2* ri = reinterpret_cast<const hf_f2*>(s_ti + j * HF_WJ + rx * HF_WP);
+        hf_f2 w[HF_W];   // (e, i) of the row's 16 cells
+#pragma unroll
+        for (int q = 0; q < HF_W / 2; ++q) {
+            const hf_f2 a = re[q], b = ri[q];
+            w[2 * q] = hf_f2{a.x, b.x};
+            w[2 * q + 1] = hf_f2{a.y, b.y};
+        }
+        hf_f2* de = reinterpret_cast<hf_f2*>(s_ye + j * HF_YJ + rx * HF_Q);
+        hf_f2* di = reinterpret_cast<hf_f2*>(s_yi + j * HF_YJ + rx * HF_Q);
+#pragma unroll
+        for (int c2 = 0; c2 < HF_Q / 2; ++c2) {
+            hf_f2 o[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+                for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[2 * c2 + h + t2];
+                o[h] = eg;
+            }
+            de[c2] = hf_f2{o[0].x, o[1].x};
+            di[c2] = hf_f2{o[0].y, o[1].y};
+        }
+    }
+    co_lds_barrier();
+    PC_STAMP(7, 3);
+
+    // 4. x pass + inhibition (:339-340): task (layer j, Q column qc) -> 10 Q values;
+    //    the partial sum over the layer's shifted own tile (Q rows/columns 3 .. 3+tw)
+    float* s_q = s_t;
+    double qs = 0.0;
+    for (int t = tid; t < TH * HF_Q; t += HF_NT) {
+        const int j = t / HF_Q, qc = t - j * HF_Q;
+        const float* ce = s_ye + j * HF_YJ + qc;
+        const float* ci = s_yi + j * HF_YJ + qc;
+        hf_f2 w[HF_W];
+#pragma unroll
+        for (int r = 0; r < HF_W; ++r) w[r] = hf_f2{ce[r * HF_Q], ci[r * HF_Q]};
+        const bool ocol = (unsigned)(qc - HALF) < (unsigned)tht;
+#pragma unroll
+        for (int qa = 0; qa < HF_Q; ++qa) {
+            hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+            for (int a = 0; a < FL; ++a) eg += gei[a] * w[qa + a];
+            const float v = (eg.x - eg.y) * k.scale;
+            const float q = (v < k.inhib) ? 0.f : v - k.inhib;
+            const bool own = ocol && (unsigned)(qa - HALF) < (unsigned)tw;
+            if (own) qs += (double)q;
+            if constexpr (EXC) {
+                if (own) Uo[((size_t)(x0 + qa - HALF) * Y + (y0 + qc - HALF)) * TH + j] = q;
+            } else {
+                s_q[j * HF_QJ + qa * HF_Q + qc] = q;
+            }
+        }
+    }
+    if constexpr (!EXC) {
+        co_lds_barrier();
+        PC_STAMP(7, 4);
+        // 5. 7 x 7 path filter (:273) + clamp (:300): task (layer j, tile column tb,
+        //    row pair ap) -> 2 outputs from 8 x 7 Q values; into [cell][3 + j] rows with
+        //    wrapped copies (layers TH-3.. before, 0..6 after), so every theta window
+        //    below is one contiguous aligned run
+        float* s_po = s_b;
+        for (int t = tid; t < TH * 8; t += HF_NT) {
+            const int j = t >> 3, tb = t & 3, ap = (t >> 2) & 1;
+            float f[FT];
+            st_filter<float>(s_ftab + s_fo[j], f);
+            float a0 = 0.f, a1 = 0.f;
+            const float* qw = s_q + j * HF_QJ + 2 * ap * HF_Q + tb;
+#pragma unroll
+            for (int r = 0; r < 2 + 2 * HALF; ++r) {  // rows of both outputs: 0..6 and 1..7
+                float w[FL];
+#pragma unroll
+                for (int y = 0; y < FL; ++y) w[y] = qw[r * HF_Q + y];
+                if (r < FL) {
+#pragma unroll
+                    for (int y = 0; y < FL; ++y) a0 += w[y] * f[r * FL + y];
+                }
+                if (r >= 1) {
+#pragma unroll
+                    for (int y = 0; y < FL; ++y) a1 += w[y] * f[(r - 1) * FL + y];
+                }
+            }
+            const float v0 = a0 > 0.f ? a0 : 0.f, v1 = a1 > 0.f ? a1 : 0.f;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float v = h ? v1 : v0;
+                float* sp = s_po + ((2 * ap + h) * HF_T + tb) * PP;
+                sp[HALF + j] = v;
+                if (j >= TH - HALF) sp[j - TH + HALF] = v;
+                if (j < FL) sp[HALF + TH + j] = v;
+            }
+        }
+        co_lds_barrier();
+        PC_STAMP(7, 5);
+        // 6. theta filter (:310) + clamp (:314): task (cell, group of 4 layers) -> one
+        //    16-byte write-through store of U (normalised by the next launch)
+        const int nbytes = (int)min((size_t)X * Y * TH * sizeof(float), (size_t)INT_MAX);
+        const bool wt = (size_t)X * Y * TH * sizeof(float) <= (size_t)INT_MAX;
+        for (int t = tid; t < HF_T * HF_T * NV; t += HF_NT) {
+            const int cell = t / NV, g = t - cell * NV, ta = cell >> 2, tb = cell & 3;
+            if (ta >= tw || tb >= tht) continue;
+            const co_f4* sv = reinterpret_cast<const co_f4*>(s_po + cell * PP + 4 * g);
+            float r[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const co_f4 x = sv[q];
+#pragma unroll
+                for (int w = 0; w < 4; ++w) r[4 * q + w] = x[w];
+            }
+            co_f4 v;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                float x = 0.f;
+#pragma unroll
+                for (int z = 0; z < FL; ++z) x += r[o + z] * ctl.zf[z];
+                v[o] = x > 0.f ? x : 0.f;
+            }
+            co_put(Uo, ((size_t)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g, v, wt, nbytes);
+        }
+    }
+    // the block's partial sum and argmax key
+    qs = co_wave_sum(qs);
+    if (lane == 0) s_red[wave] = qs;
+    if (want_key) {
+        bk = co_wave_max(bk);
+        if (lane == 0) s_bk[wave] = bk;
+    }
+    co_lds_barrier();
+    if (tid == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < HF_NW; ++w) s += s_red[w];
+        st_wt(&part_out[blockIdx.x], s);
+        if (want_key) {
+            for (int w = 1; w < HF_NW; ++w) bk = max(bk, s_bk[w]);
+            atomicMax(slot_prev + (blockIdx.x & (RES_SLOTS - 1)), bk);
+        }
+    }
+    PC_STAMP(7, 6);
+}
+
+// The end of a halo-form call: the normalised state P = U * (1/t) of the last step
+// (written back, so the handle's state is normalised between calls), its argmax key
+// per block into the last step's slots, optionally the float64 C-order volume into a
+// pinned host array (readback='eager'), and -- the last block to finish, told by an
+// agent-scope counter -- the keys of all nexp steps into the host result words (the
+// export kernel of the other forms, folded in: one launch fewer per call).
+__global__ __launch_bounds__(256) void pc_halo_finish(
+    const float* U, float* P,  // may be one buffer: each element is read, then written, by one thread
+    int n4, const double* __restrict__ part,
+    int npart, unsigned long long* __restrict__ slot, const unsigned long long* __restrict__ res,
+    int nexp, unsigned* __restrict__ counter, unsigned long long* __restrict__ host,
+    double* __restrict__ xp, int nbytes) {
+    __shared__ unsigned long long s_bk[4];
+    __shared__ int s_last;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const PcNorm<float> nrm(pc_partials_total(part, npart));
+    unsigned long long bk = 0ull;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    for (int i = blockIdx.x * 256 + tid; i < n4; i += gridDim.x * 256) {
+        const co_f4 u = reinterpret_cast<const co_f4*>(U)[i];
+        co_f4 p;
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            p[o] = nrm(u[o]);
+            bk = max(bk, argmax_key(p[o], 4u * (unsigned)i + o));
+        }
+        co_put(P, 4 * (size_t)i, p, true, nbytes);
+        if (xp) {
+            d2* d = reinterpret_cast<d2*>(xp + 4 * (size_t)i);
+            d[0] = d2{(double)p[0], (double)p[1]};
+            d[1] = d2{(double)p[2], (double)p[3]};
+        }
+    }
+    bk = co_wave_max(bk);
+    if (lane == 0) s_bk[wave] = bk;
+    __syncthreads();
+    if (tid == 0) {
+        bk = max(max(s_bk[0], s_bk[1]), max(s_bk[2], s_bk[3]));
+        atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
+        s_last = 0;
+        if (nexp > 0) {
+            // the key has reached memory (agent-scope atomics execute there) before
+            // this block counts itself done
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     gridDim.x - 1;
+        }
+    }
+    __syncthreads();
+    if (s_last) {
+        // every block's key is in: each step's max of its RES_SLOTS slots (sc1 loads,
+        // past this CU's L1) straight into the pinned host words
+        for (int s = wave; s < nexp; s += 4) {
+            const unsigned long long* r = res + (size_t)s * RES_SLOTS;
+            unsigned long long m = 0ull;
+#pragma unroll
+            for (int q = 0; q < RES_SLOTS / 64; ++q)
+                m = max(m, __hip_atomic_load(r + lane + 64 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            m = co_wave_max(m);
+            if (lane == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (tid == 0) st_wt(counter, 0u);  // for the next call
+    }
 }
 
 // Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
@@ -1934,12 +2442,12 @@ __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ b
                                                          unsigned long long* __restrict__ res_slot) {
     __shared__ T s_bv[NT];
     __shared__ unsigned s_bl[NT];
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     for (int i = threadIdx.x; i < nb; i += NT) {
         const T v = bmax[i];
         const unsigned l = bidx[i];
-        if (v > bv || (v == bv && l < bl)) {
+        if (pc_better(v, l, bv, bl)) {
             bv = v;
             bl = l;
         }
@@ -1951,7 +2459,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_finalize(const T* __restrict__ b
         if (threadIdx.x < s) {
             const T v = s_bv[threadIdx.x + s];
             const unsigned l = s_bl[threadIdx.x + s];
-            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+            if (pc_better(v, l, s_bv[threadIdx.x], s_bl[threadIdx.x])) {
                 s_bv[threadIdx.x] = v;
                 s_bl[threadIdx.x] = l;
             }
@@ -1969,12 +2477,12 @@ __global__ __launch_bounds__(NT) void pc_argmax_steps(const T* __restrict__ bmax
     __shared__ T s_bv[NT];
     __shared__ unsigned s_bl[NT];
     const size_t base = (size_t)blockIdx.x * nb;
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     for (int i = threadIdx.x; i < nb; i += NT) {
         const T v = bmax[base + i];
         const unsigned l = bidx[base + i];
-        if (v > bv || (v == bv && l < bl)) {
+        if (pc_better(v, l, bv, bl)) {
             bv = v;
             bl = l;
         }
@@ -1986,7 +2494,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_steps(const T* __restrict__ bmax
         if (threadIdx.x < st) {
             const T v = s_bv[threadIdx.x + st];
             const unsigned l = s_bl[threadIdx.x + st];
-            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+            if (pc_better(v, l, s_bv[threadIdx.x], s_bl[threadIdx.x])) {
                 s_bv[threadIdx.x] = v;
                 s_bl[threadIdx.x] = l;
             }
@@ -2004,7 +2512,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, 
     __shared__ T s_bv[NT];
     __shared__ unsigned s_bl[NT];
     const size_t n = (size_t)X * Y * TH;
-    T bv = T(-1);
+    T bv = -std::numeric_limits<T>::infinity();
     unsigned bl = 0xFFFFFFFFu;
     for (size_t e = blockIdx.x * (size_t)NT + threadIdx.x; e < n; e += (size_t)gridDim.x * NT) {
         const int k = (int)(e / ((size_t)X * Y));
@@ -2012,7 +2520,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, 
         const int i = rem / Y, j = rem - i * Y;
         const T v = P[e];
         const unsigned lin = thfast ? (unsigned)e : ((unsigned)i * Y + j) * TH + k;
-        if (v > bv || (v == bv && lin < bl)) {
+        if (pc_better(v, lin, bv, bl)) {
             bv = v;
             bl = lin;
         }
@@ -2024,7 +2532,7 @@ __global__ __launch_bounds__(NT) void pc_argmax_blocks(const T* __restrict__ P, 
         if (threadIdx.x < s) {
             const T v = s_bv[threadIdx.x + s];
             const unsigned l = s_bl[threadIdx.x + s];
-            if (v > s_bv[threadIdx.x] || (v == s_bv[threadIdx.x] && l < s_bl[threadIdx.x])) {
+            if (pc_better(v, l, s_bv[threadIdx.x], s_bl[threadIdx.x])) {
                 s_bv[threadIdx.x] = v;
                 s_bl[threadIdx.x] = l;
             }
@@ -2149,14 +2657,18 @@ struct rs_pc {
     SepKernel<double> kd{};
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float lastMs = 0.f;
-    bool profiling = false;
+    bool profiling = false;  // HIP events around the whole call (device_ms)
+    bool profKernels = false;  // ... and around every launch (kernel_ms; the events add gaps)
     std::vector<hipEvent_t> evPool;
     double kernelMs[2] = {0.0, 0.0};
     int tiling = 0;  // 64 / 128: row-tiled kernels for Y <= 64 / 128; 0: generic 3-D tiles
     bool streamed = false;  // layer-streaming kernels (default; RS_PC_FORM=rows|tiles|stream:BX,WR,KC)
     bool cols = false;      // column kernels (RS_PC_FORM=cols[:KC]): TX x TY tiles through KC layers;
                             // P and Q are then theta-fastest (C order (x, y, th))
-    int cgx = 0, cgy = 0;   // column tiles along x and y
+    bool halo = false;      // one launch per step (RS_PC_FORM=halo): HF_T x HF_T tiles through all
+                            // layers, the excitation recomputed on each tile's halo; P theta-fastest
+    unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
+    int cgx = 0, cgy = 0;   // column (or halo) tiles along x and y
     int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
     StreamGrid sg{};
@@ -2172,6 +2684,10 @@ struct rs_pc {
 };
 
 namespace {
+
+// P (and Q) theta-fastest, the reference's C order (x, y, th): the column and halo
+// forms; the others keep P layer-major
+inline bool pc_thfast(const rs_pc* h) { return h->cols || h->halo; }
 
 int pc_grow_steps(rs_pc* h, int n) {
     if (n <= h->ctlCap && n <= h->resCap) return RS_OK;
@@ -2285,6 +2801,101 @@ PcCtlRing make_ctl_ring(const rs_pc* h, int s, const unsigned char* ring = nullp
                      reinterpret_cast<const int*>(rec + ctl_off_oy(h)),
                      reinterpret_cast<const int*>(rec + ctl_off_f(h)),
                      reinterpret_cast<const double*>(rec + ctl_off_zf(h))};
+}
+
+void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out);
+
+// Control of step s for the halo form: the layers' centred shifts as window starts in
+// the union of the step's shifted 16 x 16 windows (the same for every block), which the
+// kernel loads first thing.
+void make_ctl_halo(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                   const double* zf, PcCtlHalo* c) {
+    const size_t b = (size_t)s * h->TH;
+    int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
+    for (int k = 0; k < h->TH; ++k) {
+        const int cx = co_centre(ox[b + k], h->X), cy = co_centre(oy[b + k], h->Y);
+        mnx = std::min(mnx, cx);
+        mxx = std::max(mxx, cx);
+        mny = std::min(mny, cy);
+        mxy = std::max(mxy, cy);
+    }
+    for (int k = 0; k < h->TH; ++k) {
+        c->sx[k] = (short)(co_centre(ox[b + k], h->X) - mnx);
+        c->sy[k] = (short)(co_centre(oy[b + k], h->Y) - mny);
+        c->fo[k] = (unsigned char)fidx[b + k];
+    }
+    for (int z = 0; z < FL; ++z) c->zf[z] = (float)zf[(size_t)s * FL + z];
+    c->ux = (short)mnx;
+    c->uy = (short)mny;
+    c->uw = (short)std::min(HF_W + mxx - mnx, h->X);
+    c->uh = (short)std::min(HF_W + mxy - mny, h->Y);
+    c->wrap = HF_W + mxx - mnx > h->X || HF_W + mxy - mny > h->Y;
+}
+
+// n steps of the halo form: n dependent launches (the state ping-pongs between P and Q,
+// the partial sums between the two halves of dPart), then pc_halo_finish (normalised
+// state, last step's argmax, every step's key to the host), one host sync.
+int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
+                const double* zf, int32_t* out_xyz) {
+    RS_TRY(pc_grow_steps(h, n));
+    const bool pk = h->profiling && h->profKernels;
+    if (pk) RS_TRY(pc_ensure_events(h, (size_t)2 * n + 2));
+    for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
+    if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
+    float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
+    const dim3 grid(h->cgx * h->cgy);
+    for (int s = 0; s < n; ++s) {
+        PcCtlHalo c;
+        make_ctl_halo(h, s, ox, oy, fidx, zf, &c);
+        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
+        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[s & 1], buf[(s + 1) & 1],
+                           h->dPart + (size_t)((s + 1) & 1) * h->nPart, s == 0 ? 0 : h->nPart,
+                           h->dPart + (size_t)(s & 1) * h->nPart,
+                           s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
+                           h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->X,
+                           h->Y, h->cgx, h->kf);
+        RS_HIP(hipGetLastError());
+        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
+    }
+    const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX;
+    const int n4 = (int)(h->n / 4);
+    const int nb = std::min(1024, (n4 + 255) / 256);
+    if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
+    hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[n & 1], buf[0], n4,
+                       h->dPart + (size_t)((n - 1) & 1) * h->nPart, h->nPart,
+                       h->dRes + (size_t)(n - 1) * RES_SLOTS, h->dRes, own_export ? n : 0, h->dCounter,
+                       h->hResDev, h->exportDev, (int)(h->n * sizeof(float)));
+    RS_HIP(hipGetLastError());
+    if (!h->dbgSkipExport && !own_export) {
+        hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
+                           h->hResDev);
+        RS_HIP(hipGetLastError());
+    }
+    h->dbgSkipExport = false;
+    if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n + 1], h->stream));
+    if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
+    RS_HIP(hipStreamSynchronize(h->stream));
+    for (int s = 0; s < n; ++s)
+        RS_CHECK(h->hRes[s] != RES_NONE, RS_ERR_HIP,
+                 "step %d of %d: its argmax key did not reach the host result buffer after the "
+                 "stream synchronised", s, n);
+    if (h->profiling) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
+    if (pk) {
+        h->kernelMs[0] = h->kernelMs[1] = 0.0;
+        for (int s = 0; s < n; ++s) {
+            float a = 0.f;
+            RS_HIP(hipEventElapsedTime(&a, h->evPool[2 * s], h->evPool[2 * s + 1]));
+            h->kernelMs[0] += a;
+        }
+        float b = 0.f;
+        RS_HIP(hipEventElapsedTime(&b, h->evPool[2 * n], h->evPool[2 * n + 1]));
+        h->kernelMs[1] = b;
+    } else {
+        h->lastMs = 0.f;
+    }
+    if (out_xyz)
+        for (int s = 0; s < n; ++s) decode_xyz(h, h->hRes[s], out_xyz + 3 * (size_t)s);
+    return RS_OK;
 }
 
 // Streaming variants instantiated: (BX rows per wave, WR row groups, WC column tiles of 64).
@@ -2453,6 +3064,7 @@ void decode_xyz(const rs_pc* h, unsigned long long key, int32_t* out) {
 int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                   const double* zf, int32_t* out_xyz) {
     if (n == 0) return RS_OK;
+    if (h->halo) return pc_run_halo(h, n, ox, oy, fidx, zf, out_xyz);
     RS_TRY(pc_grow_steps(h, n));
     // Batches: the column form takes each step's control as kernel arguments too (its
     // path kernel then starts its window loads without a global round trip for the
@@ -2469,10 +3081,11 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
                               h->stream));
     }
-    if (h->profiling) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
+    const bool pk = h->profiling && h->profKernels;
+    if (pk) RS_TRY(pc_ensure_events(h, (size_t)4 * n));
     if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
     for (int s = 0; s < n; ++s) {
-        const int pb = h->profiling ? 4 * s : -1;
+        const int pb = pk ? 4 * s : -1;
         if (inline_ctl) {
             PcCtlInline c;
             make_ctl_inline(h, s, ox, oy, fidx, zf, &c);
@@ -2504,10 +3117,10 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
         if (h->prec == RS_PREC_F32)
             hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const float*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)h->cols);
+                               static_cast<const float*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h));
         else
             hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const double*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)h->cols);
+                               static_cast<const double*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h));
         RS_HIP(hipGetLastError());
     }
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
@@ -2518,7 +3131,7 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
                  "stream synchronised", s, n);
     if (h->profiling) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     else h->lastMs = 0.f;  // the step-bracketing events are recorded only while profiling
-    if (h->profiling) {
+    if (pk) {
         h->kernelMs[0] = h->kernelMs[1] = 0.0;
         for (int s = 0; s < n; ++s) {
             float a = 0.f, b = 0.f;
@@ -2573,6 +3186,13 @@ int pc_odom_control(const OdoTables* h, double vtrans, double vrot, int32_t* ox,
         rows[k] = h->keyRows[(int)key - h->keyMin];
     }
     const double zo = std::floor(vr + 0.5);
+    if (!std::isfinite(zo)) {
+        // Python 2's math.floor returns a NaN or infinite argument as it is, and the
+        // theta filter built on it is all NaN (filters.theta_filter): the reference runs
+        // on with a NaN volume (posecell_network.py:304-310)
+        for (int t = 0; t < FL; ++t) zf[t] = std::numeric_limits<double>::quiet_NaN();
+        return RS_OK;
+    }
     if (!(zo >= h->zMin && zo < h->zMin + h->nZ)) return RS_ERR_CTL_RANGE;
     const double* f = h->zfTab + (size_t)((int)zo - h->zMin) * FL;
     for (int t = 0; t < FL; ++t) zf[t] = f[t];
@@ -2584,7 +3204,7 @@ int pc_argmax_impl(rs_pc* h, int32_t* out) {
     const int nb = h->nBmaxCap < 1024 ? h->nBmaxCap : 1024;
     hipLaunchKernelGGL((pc_argmax_blocks<T>), dim3(nb), dim3(NT), 0, h->stream,
                        static_cast<const T*>(h->dP), h->X, h->Y, h->TH, static_cast<T*>(h->dBmax),
-                       h->dBidx, (int)h->cols);
+                       h->dBidx, (int)pc_thfast(h));
     RS_HIP(hipGetLastError());
     hipLaunchKernelGGL((pc_argmax_finalize<T>), dim3(1), dim3(NT), 0, h->stream,
                        static_cast<const T*>(h->dBmax), h->dBidx, nb, h->dRes);
@@ -2615,9 +3235,9 @@ __global__ void pc_scale_kernel(T* __restrict__ P, size_t n, const double* __res
     for (int i = threadIdx.x; i < npart; i += NT) t += part[i];
     t = block_sum(t, s_red);
     if (t == 0.0) return;
-    const T tt = (T)t;
+    const PcNorm<T> nrm(t);
     for (size_t e = blockIdx.x * (size_t)NT + threadIdx.x; e < n; e += (size_t)gridDim.x * NT)
-        P[e] = P[e] / tt;
+        P[e] = nrm(P[e]);
 }
 
 // Step-kernel form.  Default: rows below ST_MIN_CELLS; above it the column form
@@ -2683,9 +3303,31 @@ int pc_cols_set(rs_pc* h, int kc) {
     return RS_OK;
 }
 
+// The halo form's limits: float32, the instantiated theta extent, the 16 x 16 layer
+// windows without self-overlap, the filter table in LDS, 32-bit buffer offsets.
+bool pc_halo_fit(const rs_pc* h) {
+    return h->esz == 4 && h->TH == HF_TH && h->X >= HF_W && h->Y >= HF_W && h->nf <= RT_NFMAX &&
+           h->n * sizeof(float) <= (size_t)INT_MAX;
+}
+
+int pc_halo_set(rs_pc* h) {
+    h->streamed = false;
+    h->cols = false;
+    h->halo = true;
+    h->cgx = (h->X + HF_T - 1) / HF_T;
+    h->cgy = (h->Y + HF_T - 1) / HF_T;
+    return RS_OK;
+}
+
 int pc_choose_form(rs_pc* h) {
     int bx = 1, wr = 8, wc = 1, kc = 0;
     const char* env = std::getenv("RS_PC_FORM");
+    if (env && std::strcmp(env, "halo") == 0) {
+        RS_CHECK(pc_halo_fit(h), RS_ERR_ARG,
+                 "RS_PC_FORM=halo needs float32, TH == %d, X and Y >= %d and at most %d path filters", HF_TH,
+                 HF_W, RT_NFMAX);
+        return pc_halo_set(h);
+    }
     if (env && std::strcmp(env, "rows") == 0) {
         RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=rows needs Y <= 128");
         h->streamed = false;
@@ -2710,7 +3352,7 @@ int pc_choose_form(rs_pc* h) {
         RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | tiles | cols | stream[:BX,WR,WC[,KC]])", env);
+                 "unknown RS_PC_FORM '%s' (rows | tiles | cols | halo | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
@@ -2810,7 +3452,10 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         delete h;
         return st;
     }
-    if (h->cols) {
+    if (h->halo) {
+        h->nPart = h->cgx * h->cgy;
+        h->nPathBlocks = h->nPart;
+    } else if (h->cols) {
         h->nPart = h->cgx * h->cgy * h->coNch;
         h->nPathBlocks = h->nPart;
     } else if (h->streamed) {
@@ -2844,8 +3489,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     // kernel reads them; zeroed anyway so that no launch can see a freed handle's data
     // (rs_pc_debug(RS_PC_DBG_POISON) + tests/test_posecell_gpu.py check the former)
     PC_ALLOC(hipMemsetAsync(h->dQ, 0, h->n * h->esz, h->stream));
-    PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart));
-    PC_ALLOC(hipMemsetAsync(h->dPart, 0, sizeof(double) * h->nPart, h->stream));
+    // (the halo form keeps two steps' partial sums: the one it reads, the one it writes)
+    PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart * 2));
+    PC_ALLOC(hipMemsetAsync(h->dPart, 0, sizeof(double) * h->nPart * 2, h->stream));
+    PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
+    PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
@@ -2878,7 +3526,7 @@ int rs_pc_destroy(rs_pc* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->hRead) (void)hipHostFree(h->hRead);
-    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, h->dBmax, (void*)h->dBidx, h->dArgV,
+    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, (void*)h->dCounter, h->dBmax, (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
         if (p) (void)hipFree(p);
@@ -2916,7 +3564,19 @@ int rs_pc_excite(rs_pc* h) {
     rs::clear_error();
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
-    if (h->prec == RS_PREC_F32) {
+    if (h->halo) {
+        // the halo kernel's excitation-only instance: no shifts, Q of the own cells
+        PcCtlHalo c{};
+        c.uw = (short)HF_W;
+        c.uh = (short)HF_W;
+        hipLaunchKernelGGL((pc_step_halo<true>), dim3(h->cgx * h->cgy), dim3(HF_NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), static_cast<float*>(h->dQ), h->dPart, 0, h->dPart,
+                           nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->X, h->Y, h->cgx,
+                           h->kf);
+        RS_HIP(hipGetLastError());
+        hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
+                           static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
+    } else if (h->prec == RS_PREC_F32) {
         RS_TRY((pc_launch_step<float, PcCtlRing>(h, step_out(h, 0), nullptr, -1)));
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
@@ -3061,7 +3721,7 @@ int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th) {
              "inject location (%d, %d, %d) outside grid (%d, %d, %d)", x, y, th, h->X, h->Y, h->TH);
     RS_HIP(hipSetDevice(h->device));
     // the column form keeps P theta-fastest (C order); the others layer-major
-    const size_t idx = h->cols ? ((size_t)x * h->Y + y) * h->TH + th : ((size_t)th * h->X + x) * h->Y + y;
+    const size_t idx = pc_thfast(h) ? ((size_t)x * h->Y + y) * h->TH + th : ((size_t)th * h->X + x) * h->Y + y;
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_inject_kernel<float>), dim3(1), dim3(64), 0, h->stream,
                            static_cast<float*>(h->dP), idx, energy);
@@ -3101,10 +3761,10 @@ int rs_pc_read(rs_pc* h, double* host) {
     const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_export_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
     else
         hipLaunchKernelGGL((pc_export_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
     RS_HIP(hipGetLastError());
     if (dma) RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
@@ -3122,10 +3782,10 @@ int rs_pc_read_pinned(rs_pc* h, double* pinned) {
     const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
     else
         hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
     RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
@@ -3138,10 +3798,10 @@ int rs_pc_write(rs_pc* h, const double* host) {
     RS_HIP(hipMemcpyAsync(h->dTmp, host, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_import_kernel<float>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
-                           static_cast<float*>(h->dP), h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<float*>(h->dP), h->X, h->Y, h->TH, (int)pc_thfast(h));
     else
         hipLaunchKernelGGL((pc_import_kernel<double>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
-                           static_cast<double*>(h->dP), h->X, h->Y, h->TH, (int)h->cols);
+                           static_cast<double*>(h->dP), h->X, h->Y, h->TH, (int)pc_thfast(h));
     RS_HIP(hipGetLastError());
     RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
@@ -3171,7 +3831,9 @@ int rs_pc_last_ms(rs_pc* h, double* ms) {
 
 int rs_pc_set_profiling(rs_pc* h, int enable) {
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
+    // 1: events around every launch too (kernel_ms); 2: around the whole call only
     h->profiling = enable != 0;
+    h->profKernels = enable == 1;
     return RS_OK;
 }
 
@@ -3185,6 +3847,7 @@ int rs_pc_kernel_ms(rs_pc* h, double ms[2]) {
 const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
     if (h->streamed) return "stream";
+    if (h->halo) return "halo";
     if (h->cols) return "cols";
     return h->tiling ? "rows" : "tiles";
 }
@@ -3197,7 +3860,7 @@ int rs_pc_debug(rs_pc* h, int op) {
         // every buffer a step writes before it reads: all bits set (NaN volumes, the
         // largest possible argmax key in every slot of every step)
         RS_HIP(hipMemsetAsync(h->dQ, 0xFF, h->n * h->esz, h->stream));
-        RS_HIP(hipMemsetAsync(h->dPart, 0xFF, sizeof(double) * h->nPart, h->stream));
+        RS_HIP(hipMemsetAsync(h->dPart, 0xFF, sizeof(double) * h->nPart * 2, h->stream));
         RS_HIP(hipMemsetAsync(h->dRes, 0xFF, sizeof(unsigned long long) * RES_SLOTS * h->resCap, h->stream));
         RS_HIP(hipMemsetAsync(h->dBmax, 0xFF, h->esz * h->nBmaxCap, h->stream));
         RS_HIP(hipMemsetAsync(h->dBidx, 0xFF, sizeof(unsigned) * h->nBmaxCap, h->stream));

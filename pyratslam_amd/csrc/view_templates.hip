@@ -557,22 +557,27 @@ struct PlaneLds {
 // planes and adds its partial counts into part[i&1] while batch i+1 is staged into
 // the other plane buffer; one barrier per batch.  Each buffer is its own
 // namespace-scope __shared__ variable and every access names one of them at
-// compile time (pl_q<CUR>, pl_part<CUR>): hipcc waits for an LDS-DMA in flight
+// compile time (pl_q<H, CUR>, pl_part<CUR>): hipcc waits for an LDS-DMA in flight
 // before any LDS access it cannot prove disjoint from the DMA's variable, so
 // only distinct, statically named variables let the next batch's DMA stay in
 // flight through this batch's compute.
-constexpr int PL_NK = PlaneLds<64>::NK;
-constexpr int PL_QP = PlaneLds<64>::QP;   // H = 64 is the larger instantiation
-__shared__ uint4 vt_pl_qa[PL_QP];         // staged query planes, even batches
-__shared__ uint4 vt_pl_qb[PL_QP];         // odd batches
+constexpr int PL_NK = PlaneLds<64>::NK;   // the same for every H (it depends on max_offset only)
+static_assert(PlaneLds<32>::NK == PL_NK, "partial-count slots independent of H");
+// the staged query planes, sized per template height (a kernel allocates only the
+// instances it names: the H = 32 scan, the ROS node's geometry, does not carry the
+// H = 64 buffers)
+template <int H>
+__shared__ uint4 vt_pl_qa[PlaneLds<H>::QP];   // even batches
+template <int H>
+__shared__ uint4 vt_pl_qb[PlaneLds<H>::QP];   // odd batches
 __shared__ uint32_t vt_pl_part0[PL_NB][PL_NK][64];  // u16 pairs of partial counts, summed by ds_add
 __shared__ uint32_t vt_pl_part1[PL_NB][PL_NK][64];
 __shared__ int vt_pl_bidx[3];             // batches taken ahead (ring)
 __shared__ uint32_t vt_pl_ts[16][64];     // TS(o) of the block's 64 templates
-template <int CUR>
+template <int H, int CUR>
 __device__ __forceinline__ uint4* pl_q() {
-    if constexpr (CUR == 0) return vt_pl_qa;
-    else return vt_pl_qb;
+    if constexpr (CUR == 0) return vt_pl_qa<H>;
+    else return vt_pl_qb<H>;
 }
 template <int CUR>
 __device__ __forceinline__ uint32_t (&pl_part())[PL_NB][PL_NK][64] {
@@ -618,8 +623,8 @@ __device__ __forceinline__ bool plane_batch(const uint32_t (&P)[PlaneRange<H, HA
     using LD = PlaneLds<H>;
     constexpr int NO = LD::NO, NK = LD::NK, NS = LD::NS, NT = 64 * LD::NW;
     if (bi >= nbatch) return false;  // block-uniform
-    const uint4* qcur = pl_q<CUR>();
-    uint4* qnxt = pl_q<CUR ^ 1>();
+    const uint4* qcur = pl_q<H, CUR>();
+    uint4* qnxt = pl_q<H, CUR ^ 1>();
     uint32_t(&part)[PL_NB][PL_NK][64] = pl_part<CUR>();
     const int tid = wave * 64 + lane;
     // batch ring: iteration it reads the next batch from slot (it+1) % 3 and thread
@@ -757,7 +762,7 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
         constexpr int QW4 = PlaneLds<H>::QW / 4;
         const int qb = (vt_pl_bidx[0] * G + g) * PL_NB, nb = min(PL_NB, nq - qb);
         const uint4* qp4 = reinterpret_cast<const uint4*>(qp);
-        for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) vt_pl_qa[i] = qp4[(size_t)qb * QW4 + i];
+        for (int i = threadIdx.x; i < nb * QW4; i += blockDim.x) vt_pl_qa<H>[i] = qp4[(size_t)qb * QW4 + i];
     }
     __syncthreads();
     const uint4* qp4 = reinterpret_cast<const uint4*>(qp);

@@ -148,32 +148,76 @@ def layer_trig(th):
     return t
 
 
+def _layer_key_error(resid):
+    """The exception the reference's per-layer LUT lookup raises first, in layer order
+    (posecell_network.py:244-250: ``filter_dict_2d[(int(r * prec), int(r * prec))]``), or
+    None: ``int`` of a NaN residual raises ValueError, of an infinite one OverflowError
+    (Python 2 and 3 alike), a finite key outside the table KeyError((k, k)).  A NaN
+    residual is what a non-finite vtrans gives: ``inf - around(inf)`` is NaN."""
+    for r in resid:
+        if math.isnan(r):
+            return ValueError('cannot convert float NaN to integer')
+        if math.isinf(r):
+            return OverflowError('cannot convert float infinity to integer')
+        k = int(r)
+        if not (LUT_KEYS.start <= k < LUT_KEYS.stop):
+            return KeyError((k, k))
+    return None
+
+
+NAN_FILTER_1D = np.full(FILTER_LEN, np.nan)
+NAN_FILTER_1D.setflags(write=False)
+
+
+def theta_filter(vr):
+    """diff_gaussian_offset_1d(origin=floor(vr + .5)) (posecell_network.py:304-308).  Under
+    Python 2 ``math.floor`` of a NaN or infinite argument returns it as a float, and the
+    filter built on it is all NaN (``exp`` of NaN, or 0/0 in the normalisation): the
+    reference runs on with a NaN volume instead of raising."""
+    zo = vr + .5
+    if not math.isfinite(zo):
+        return NAN_FILTER_1D
+    return filter_1d(math.floor(zo))
+
+
 def step_control(vtrans, vrot, th, table):
     """Per-step control of path_integration (posecell_network.py:252-308).
 
     Returns (ox, oy, rows, zf, radius) with ox/oy/rows int32[th], zf float64[7].
     Same NumPy operations on the same operands as the reference, so bit-identical.
+    Raises what the reference raises at its LUT lookup (:249): KeyError((k, k)) for a
+    key outside the table, ValueError for a non-finite vtrans.
     """
     vrot_scale = 2.0 * np.pi / th
     vt = vtrans / PC_CELL_X_SIZE
     vr = vrot / vrot_scale
     cos_a, sin_a = layer_trig(th)
-    ex = vt * cos_a
-    ey = vt * sin_a
-    rx = np.around(ex)
-    ry = np.around(ey)
-    keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)   # int() truncates
+    with np.errstate(invalid='ignore', over='ignore'):
+        ex = vt * cos_a
+        ey = vt * sin_a
+        rx = np.around(ex)
+        ry = np.around(ey)
+        resid = (ex - rx) * LUT_PRECISION
+    if not np.isfinite(resid).all() or resid.min() < LUT_KEYS.start or resid.max() >= LUT_KEYS.stop:
+        err = _layer_key_error(resid)
+        if err is not None:
+            raise err
+    keys = np.trunc(resid).astype(np.int64)   # int() truncates
     rows = table.rows_for_keys(keys)
-    zf = filter_1d(math.floor(vr + .5))
+    zf = theta_filter(vr)
     radius = int(np.ceil(abs(vt)))
-    return rx.astype(np.int32), ry.astype(np.int32), rows, zf, radius
+    # shifts beyond int32 (|vtrans| above ~4e8 m per step) saturate instead of wrapping
+    # through a cast warning; the reference would fail allocating a halo of that radius
+    lim = np.iinfo(np.int32)
+    return (np.clip(rx, lim.min, lim.max).astype(np.int32), np.clip(ry, lim.min, lim.max).astype(np.int32),
+            rows, zf, radius)
 
 
 def batch_control(odometry, th, table):
     """step_control for n steps at once (vectorised over steps).
 
     Returns (ox, oy, rows, zf) shaped (n, th), (n, th), (n, th), (n, 7) and the
-    index of the first step whose LUT key is invalid (or None): steps before it
+    index of the first step whose LUT lookup raises (or None): steps before it
     are valid, matching the point where the reference would raise.
     """
     od = np.asarray(odometry, dtype=np.float64).reshape(-1, 2)
@@ -182,20 +226,29 @@ def batch_control(odometry, th, table):
     vt = od[:, 0] / PC_CELL_X_SIZE
     vr = od[:, 1] / vrot_scale
     cos_a, sin_a = layer_trig(th)
-    ex = vt[:, None] * cos_a[None, :]
-    ey = vt[:, None] * sin_a[None, :]
-    rx = np.around(ex)
-    ry = np.around(ey)
-    keys = np.trunc((ex - rx) * LUT_PRECISION).astype(np.int64)
-    bad = ((keys < LUT_KEYS.start) | (keys >= LUT_KEYS.stop)).any(axis=1)
+    with np.errstate(invalid='ignore', over='ignore'):
+        ex = vt[:, None] * cos_a[None, :]
+        ey = vt[:, None] * sin_a[None, :]
+        rx = np.around(ex)
+        ry = np.around(ey)
+        resid = (ex - rx) * LUT_PRECISION
+    bad = (~np.isfinite(resid)).any(axis=1)
+    keys = np.trunc(np.where(np.isfinite(resid), resid, 0.0)).astype(np.int64)
+    bad |= ((keys < LUT_KEYS.start) | (keys >= LUT_KEYS.stop)).any(axis=1)
     first_bad = int(np.argmax(bad)) if bad.any() else None
     keys = np.clip(keys, LUT_KEYS.start, LUT_KEYS.stop - 1)
     rows = table._key_to_row[keys - LUT_KEYS.start]
-    zorig = np.floor(vr + .5).astype(np.int64)
     zf = np.empty((n, FILTER_LEN))
-    for o in np.unique(zorig):
-        zf[zorig == o] = filter_1d(int(o))
-    return (rx.astype(np.int32), ry.astype(np.int32), rows.astype(np.int32), zf, first_bad)
+    zo = vr + .5
+    fin = np.isfinite(zo)
+    zf[~fin] = np.nan
+    zorig = np.floor(np.where(fin, zo, 0.0)).astype(np.int64)
+    for o in np.unique(zorig[fin]):
+        zf[fin & (zorig == o)] = filter_1d(int(o))
+    lim = np.iinfo(np.int32)
+    ox = np.clip(np.where(np.isfinite(rx), rx, 0), lim.min, lim.max).astype(np.int32)
+    oy = np.clip(np.where(np.isfinite(ry), ry, 0), lim.min, lim.max).astype(np.int32)
+    return (ox, oy, rows.astype(np.int32), zf, first_bad)
 
 
 ZORIG_MARGIN = 8

@@ -52,7 +52,9 @@ class _PinnedArrays:
         self._lib, self._n, self._cap = lib, n, cap
         self._free = []
         self._blocks = 0
-        self._lock = threading.Lock()
+        # reentrant: a cyclic GC run inside a locked section can finalise one of this
+        # pool's arrays on the same thread, and _release takes the lock again
+        self._lock = threading.RLock()
 
     def array(self, shape):
         with self._lock:
@@ -83,9 +85,10 @@ class _PinnedArrays:
     _closed = False
 
     def close(self):
+        empty = []   # allocated before the lock is taken
         with self._lock:
             self._closed = True
-            free, self._free = self._free, []
+            free, self._free = self._free, empty
         for ptr in free:
             self._lib.rs_host_free(ctypes.c_void_p(ptr))
 
@@ -363,11 +366,13 @@ class PoseCellNetwork:
         return ms.value
 
     def step_form(self):
-        """Step kernels in use: 'rows', 'tiles', 'cols' or 'stream' (rs_pc_step_form)."""
+        """Step kernels in use: 'rows', 'tiles', 'cols', 'halo' or 'stream' (rs_pc_step_form)."""
         return self._lib.rs_pc_step_form(self._h).decode()
 
-    def set_profiling(self, enable=True):
-        _lib.check(self._lib.rs_pc_set_profiling(self._h, int(bool(enable))))
+    def set_profiling(self, enable=True, per_kernel=True):
+        """HIP events around each update()/run() (device_ms) and, with per_kernel, around
+        every launch too (kernel_ms; those events add gaps between the kernels)."""
+        _lib.check(self._lib.rs_pc_set_profiling(self._h, 0 if not enable else (1 if per_kernel else 2)))
 
     def kernel_ms(self):
         """(excite_ms, path_ms) summed over the steps of the last run (profiling on)."""

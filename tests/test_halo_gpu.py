@@ -1,0 +1,250 @@
+"""The halo form (RS_PC_FORM=halo): one launch per pose-cell step, the excitation
+recomputed on each tile's halo and the state carried unnormalised between the
+launches of a call (posecell.hip, pc_step_halo / pc_halo_finish).  Checked against
+the reference-made golden trajectories and the float64 oracle: float32 activations
+within 1e-5 (BASELINE.json north_star), argmax identical at every step, and the
+peak returned always the argmax of the handle's own state."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import dense_state, load_golden
+from oracle import posecell as P
+
+pytestmark = pytest.mark.gpu
+
+F32_TOL = 1e-5
+
+
+@pytest.fixture(scope='module')
+def pcn():
+    from pyratslam_amd import _build
+    _build.build()
+    from pyratslam_amd import PoseCellNetwork
+    return PoseCellNetwork
+
+
+@pytest.fixture
+def halo(monkeypatch, pcn):
+    monkeypatch.setenv('RS_PC_FORM', 'halo')
+
+    def make(shape, **kw):
+        net = pcn(shape, **kw)
+        assert net.step_form() == 'halo'
+        return net
+    return make
+
+
+def odometry(n, seed, vmax=0.6, rmax=0.15):
+    r = np.random.default_rng(seed)
+    return np.stack([r.uniform(0, vmax, n), r.uniform(-rmax, rmax, n)], axis=1)
+
+
+def own_argmax(net):
+    p = net.posecells
+    return tuple(int(v) for v in np.unravel_index(np.argmax(p), p.shape)), p
+
+
+@pytest.mark.parametrize('name', ['pc64_s0', 'pc_ros21'])
+def test_golden_trajectory_per_step_and_batched(halo, name):
+    case = load_golden(name)
+    shape = tuple(int(s) for s in case['shape'])
+    net = halo(shape)
+    net.inject(1, tuple(case['inject']))
+    for s, v in enumerate(case['odom']):
+        m = net.update(v)
+        assert m == tuple(case['max_pc'][s]), (name, s)
+        own, p = own_argmax(net)
+        assert own == m, (name, s)
+        assert np.abs(p - dense_state(case, s)).max() < F32_TOL, (name, s)
+    b = halo(shape)
+    b.inject(1, tuple(case['inject']))
+    n = len(case['odom'])
+    got = np.concatenate([b.run(case['odom'][:n // 3]), b.run(case['odom'][n // 3:])])
+    assert np.array_equal(got, case['max_pc'])
+    assert np.abs(b.posecells - dense_state(case, n - 1)).max() < F32_TOL
+
+
+def test_network_death_vs_reference(halo):
+    """pc_death64 (made by the reference): the dead steps take the total == 0
+    branch and stay exactly zero, the peak of the all-zero volume is (0, 0, 0), a
+    second inject revives it; per step and batched around the inject."""
+    case = load_golden('pc_death64')
+    shape = tuple(int(s) for s in case['shape'])
+    kill, revive = int(case['kill_step']), int(case['revive_step'])
+    odom = case['odom']
+    net = halo(shape)
+    net.inject(1, tuple(case['inject']))
+    for s, v in enumerate(odom):
+        if s == revive:
+            net.inject(1, tuple(int(c) for c in case['revive']))
+        m = net.update(v)
+        assert m == tuple(case['max_pc'][s]), (s, m)
+        assert net.get_pc_max() == tuple(case['get_pc_max'][s])
+        p = net.posecells
+        if kill <= s < revive:
+            assert not p.any(), s
+        assert np.abs(p - dense_state(case, s)).max() < F32_TOL, s
+    b = halo(shape)
+    b.inject(1, tuple(case['inject']))
+    m1 = b.run(odom[:revive])
+    b.inject(1, tuple(int(c) for c in case['revive']))
+    m2 = b.run(odom[revive:])
+    assert np.array_equal(np.concatenate([m1, m2]), case['max_pc'])
+    assert np.abs(b.posecells - dense_state(case, len(odom) - 1)).max() < F32_TOL
+
+
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (17, 30, 36), (16, 16, 36)])
+def test_random_and_fast_odometry_vs_oracle(halo, shape):
+    """Bench odometry mixed with fast steps (vtrans up to 2 m: shifts up to 10 cells,
+    unions beyond the LDS-DMA image, which take the direct-load path), ragged tiles
+    (17 x 30) and a grid of exactly one window (16 x 16); run() in batches of 7 so
+    every batch starts from a normalised state and ends in pc_halo_finish."""
+    r = np.random.default_rng(41)
+    n = 28
+    od = np.stack([np.where(r.random(n) < 0.6, r.uniform(0, 0.6, n), r.uniform(0.9, 2.0, n)),
+                   r.uniform(-0.15, 0.15, n)], axis=1)
+    net = halo(shape)
+    ref = P.PoseCellOracle(shape)
+    loc = tuple(s // 2 for s in shape)
+    net.inject(1, loc)
+    ref.inject(1, loc)
+    got = np.concatenate([net.run(od[i:i + 7]) for i in range(0, n, 7)])
+    for s in range(n):
+        assert tuple(got[s]) == ref.update(od[s]), (shape, s)
+    own, p = own_argmax(net)
+    assert own == tuple(got[-1])
+    assert np.abs(p - ref.posecells).max() < F32_TOL
+
+
+def _oracle_step_with_control(ref, ox, oy, rows, zf, table):
+    ref.excite_inhibit_normalise()
+    filters = np.moveaxis(table[rows], 0, -1)
+    p = P.conv_xy_shift(ref.posecells, ox, oy, filters)
+    p[p < 0] = 0
+    p = P.conv_z_wrap(p, zf)
+    p[p < 0] = 0
+    ref.posecells = p
+    return ref.get_pc_max()
+
+
+def test_uniform_large_shift_own_tile_outside_union(halo):
+    """Every layer shifted by the same 9 cells (explicit control through
+    rs_pc_update): the union of the step's windows no longer holds a tile's own
+    cells, whose argmax keys then come from memory."""
+    shape = (64, 64, 36)
+    net = halo(shape)
+    ref = P.PoseCellOracle(shape)
+    for x in (net, ref):
+        x.inject(1, (32, 32, 18))
+    table = net._table
+    zf = np.ascontiguousarray(P.dog_offset_1d(0), dtype=np.float64)
+    for s, (sx, sy) in enumerate([(9, 9), (-9, 5), (9, -12), (0, 0)]):
+        ox = np.full(36, sx, dtype=np.int32)
+        oy = np.full(36, sy, dtype=np.int32)
+        rows = np.full(36, net.filter_table.index[(0, 0)], dtype=np.int32)
+        want = _oracle_step_with_control(ref, ox, oy, rows, zf, table)
+        st = net._update(net._h, ox.ctypes.data, oy.ctypes.data, rows.ctypes.data, zf.ctypes.data,
+                         net._out3_addr)
+        assert st == 0
+        assert tuple(int(v) for v in net._out3) == want, s
+    # the next update() re-reads the state the uniform steps left
+    v = (0.3, 0.05)
+    assert net.update(v) == ref.update(v)
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+
+
+def test_poisoned_scratch_first_updates_vs_c_oracle(halo):
+    from oracle import c_oracle as C
+    from pyratslam_amd import _lib
+    shape = (64, 64, 36)
+    od = odometry(4, 31)
+    ref = C.PoseCellC(shape)
+    ref.inject(1, (32, 32, 18))
+    want = [ref.update(v) for v in od]
+    for batched in (False, True):
+        net = halo(shape)
+        _lib.check(net._lib.rs_pc_debug(net._h, _lib.RS_PC_DBG_POISON))
+        net.inject(1, (32, 32, 18))
+        got = [tuple(r) for r in net.run(od)] if batched else [net.update(v) for v in od]
+        assert got == want, batched
+        p = net.posecells
+        assert np.isfinite(p).all()
+        assert np.abs(p - ref.posecells).max() < F32_TOL
+        net.close()
+
+
+def test_keyerror_leaves_reference_state(halo):
+    """vtrans 0.1 m = half a cell: the layer at heading 0 has residual +0.5, key 5,
+    the reference's KeyError((5, 5)) after steps 1-4 (posecell_network.py:249)."""
+    shape = (64, 64, 36)
+    net = halo(shape)
+    net.inject(1, (32, 32, 18))
+    with pytest.raises(KeyError) as e:
+        net.update((0.1, 0.0))
+    assert e.value.args[0] == (5, 5)
+    ref = P.PoseCellOracle(shape)
+    ref.inject(1, (32, 32, 18))
+    ref.excite_inhibit_normalise()
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+    net2 = halo(shape)
+    net2.inject(1, (32, 32, 18))
+    with pytest.raises(KeyError):
+        net2.run([[0.2, 0.0], [0.3, 0.01], [0.1, 0.0]])
+    ref2 = P.PoseCellOracle(shape)
+    ref2.inject(1, (32, 32, 18))
+    ref2.update((0.2, 0.0))
+    ref2.update((0.3, 0.01))
+    ref2.excite_inhibit_normalise()
+    assert np.abs(net2.posecells - ref2.posecells).max() < F32_TOL
+
+
+def test_long_run_export_and_eager_readback(halo, pcn, monkeypatch):
+    """A run() longer than pc_halo_finish exports itself (the separate export kernel
+    then returns the keys) equals update() per step, and equals the rows form; the
+    eager readback (the float64 volume written by pc_halo_finish) equals the lazy
+    one; the export sentinel still fails a step whose key never arrived."""
+    from pyratslam_amd import _lib
+    shape = (64, 64, 36)
+    od = odometry(150, 12)
+    a, b = halo(shape), halo(shape, readback='eager')
+    for n in (a, b):
+        n.inject(1, (32, 32, 18))
+    ma = a.run(od)
+    for s, v in enumerate(od):
+        assert b.update(v) == tuple(ma[s]), s
+        if s % 25 == 0:
+            assert np.array_equal(b.posecells, b.posecells.copy())
+    pa = a.posecells
+    assert np.array_equal(b.posecells, pa)
+    monkeypatch.setenv('RS_PC_FORM', 'rows')
+    c = pcn(shape)
+    assert c.step_form() == 'rows'
+    c.inject(1, (32, 32, 18))
+    assert np.array_equal(c.run(od), ma)
+    assert np.abs(c.posecells - pa).max() < 1e-6
+    _lib.check(a._lib.rs_pc_debug(a._h, _lib.RS_PC_DBG_SKIP_EXPORT))
+    with pytest.raises(_lib.HipLibraryError, match='did not reach'):
+        a.update(od[0])
+    assert a.update(od[1]) == own_argmax(a)[0]
+
+
+def test_state_roundtrip_inject_argmax_total(halo):
+    shape = (21, 21, 36)
+    rng = np.random.default_rng(3)
+    net = halo(shape)
+    assert (net.posecells == 0).all()
+    assert net.get_pc_max() == (0, 0, 0)
+    v = rng.random(shape)
+    net.posecells = v
+    back = net.posecells
+    assert np.array_equal(back, v.astype(np.float32).astype(np.float64))
+    assert net.get_pc_max() == tuple(np.unravel_index(np.argmax(back), shape))
+    net.inject(5.0, (3, 4, 5))
+    assert net.get_pc_max() == (3, 4, 5)
+    assert abs(net.total() - back.sum() - 5.0) < 1e-6 * back.size
+    buf = np.empty(shape)
+    from pyratslam_amd import _lib
+    _lib.check(net._lib.rs_pc_read(net._h, _lib.ptr(buf, ctypes.c_double)))
+    assert buf[3, 4, 5] == pytest.approx(back[3, 4, 5] + 5.0, rel=1e-6)

@@ -151,20 +151,20 @@ def test_library_control_bit_identical_to_numpy(th):
     live = np.stack([rng.uniform(0, 0.6, 3000), rng.uniform(-0.15, 0.15, 3000)], axis=1)
     wide = np.stack([rng.uniform(-3, 3, 3000), rng.uniform(-7, 7, 3000)], axis=1)
     od = np.concatenate([live, wide, _edge_odometry(th, 6000, th),
-                         [[0.0, 0.0], [-0.0, -0.0], [np.nan, 0.0], [0.1, np.nan], [1e300, 0.0]]])
+                         [[0.0, 0.0], [-0.0, -0.0], [np.nan, 0.0], [0.1, np.nan], [1e300, 0.0],
+                          [np.inf, 0.0], [-np.inf, 0.1], [0.3, np.nan], [0.3, np.inf], [0.25, -np.inf]]])
     ox, oy, rows, zf, st = _library_control(th, od)
     from pyratslam_amd import _lib
     n_ok = n_key = n_range = 0
     for i, (vt, vr) in enumerate(od):
         try:
             rx, ry, rr, zz, _ = F.step_control(float(vt), float(vr), th, table)
-        except (KeyError, ValueError, OverflowError) as e:
-            if isinstance(e, KeyError):
-                assert st[i] == _lib.RS_ERR_LUT_KEY, (i, vt, vr, st[i])
-                n_key += 1
-            else:   # math.floor(nan / inf): the library defers to the host path
-                assert st[i] == _lib.RS_ERR_CTL_RANGE, (i, vt, vr, st[i])
-                n_range += 1
+        except (KeyError, ValueError, OverflowError):
+            # KeyError((k, k)) for a key outside the LUT, ValueError for the NaN residual
+            # of a non-finite vtrans: the library reports both at the same layer as
+            # RS_ERR_LUT_KEY, and the wrapper re-raises the host's exception
+            assert st[i] == _lib.RS_ERR_LUT_KEY, (i, vt, vr, st[i])
+            n_key += 1
             continue
         if st[i] == _lib.RS_ERR_CTL_RANGE:
             n_range += 1
@@ -223,3 +223,36 @@ def test_pinned_pool_reuses_and_caps_blocks():
     del b, d
     gc.collect()
     assert lib.live == {}                         # released after close: freed
+
+
+@pytest.mark.parametrize('th', [18, 36])
+def test_nonfinite_odometry_like_reference(th):
+    """posecell_network.py:244-308 under Python 2, the reference's interpreter: a
+    non-finite vtrans gives NaN residuals (inf - around(inf) is NaN) and int(NaN)
+    raises ValueError at the first layer; a non-finite vrot makes math.floor return
+    it unchanged and the theta filter all NaN, with no exception.  No cast warnings."""
+    import warnings
+    table = F.FilterTable()
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        for vt in (np.nan, np.inf, -np.inf, 1e308):    # 1e308 / 0.2 overflows to inf
+            with pytest.raises(ValueError, match='NaN'):
+                F.step_control(vt, 0.0, th, table)
+            with pytest.raises(ValueError):
+                P.step_control(vt, 0.0, (8, 8, th), P.lut_2d())
+        with pytest.raises(KeyError) as e:              # a LUT miss at an earlier layer wins
+            F.step_control(0.1, np.nan, th, table)
+        assert e.value.args[0] == (5, 5)
+        for vr in (np.nan, np.inf, -np.inf):
+            ox, oy, rows, zf, _ = F.step_control(0.3, vr, th, table)
+            assert np.isnan(zf).all() and zf.shape == (7,)
+            ref = P.step_control(0.3, vr, (8, 8, th), P.lut_2d())
+            assert np.isnan(ref['zf']).all()
+            assert np.array_equal(ox, ref['ox']) and np.array_equal(oy, ref['oy'])
+        od = np.array([[0.2, 0.0], [0.3, np.nan], [np.inf, 0.0], [0.1, 0.0]])
+        ox, oy, rows, zf, first_bad = F.batch_control(od, th, table)
+        assert first_bad == 2
+        assert np.isnan(zf[1]).all() and np.isfinite(zf[0]).all()
+        assert F.batch_control(od[[0, 3]], th, table)[4] == 1          # KeyError step
+        assert F.batch_control(od[:2], th, table)[4] is None
+        F.step_control(1e12, 0.0, th, table)            # huge finite shifts: no cast warning

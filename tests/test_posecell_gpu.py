@@ -509,3 +509,45 @@ def test_large_grid_wide_shifts_vs_c_oracle(pcn, precision, tol):
         m = ref.update(v)
         assert net.update(v) == m, (s, v)
     assert np.abs(net.posecells - ref.posecells).max() < tol
+
+
+@pytest.mark.parametrize('form,precision', [('', 'float32'), ('', 'float64'), ('halo', 'float32'),
+                                            ('cols', 'float32')])
+def test_nonfinite_odometry_like_reference(pcn, monkeypatch, form, precision):
+    """posecell_network.py:244-310 under Python 2: a NaN or infinite vtrans raises
+    ValueError at the LUT lookup (int() of the NaN residual inf - around(inf)) after
+    steps 1-4 ran, per call and at the first bad step of run(); a NaN or infinite vrot
+    raises nothing (Python 2's math.floor returns it) and the all-NaN theta filter
+    leaves a NaN volume whose peak, numpy's first NaN, is (0, 0, 0), for good."""
+    monkeypatch.setenv('RS_PC_FORM', form)
+    shape = (64, 64, 36)
+    tol = F32_TOL if precision == 'float32' else F64_TOL
+    loc = (32, 32, 18)
+    for vt in (np.nan, np.inf):
+        net, ref = pcn(shape, precision=precision), P.PoseCellOracle(shape)
+        assert not form or net.step_form() == form
+        for x in (net, ref):
+            x.inject(1, loc)
+        assert net.update((0.2, 0.01)) == ref.update((0.2, 0.01))
+        with pytest.raises(ValueError):
+            net.update((vt, 0.0))
+        ref.excite_inhibit_normalise()
+        assert np.abs(net.posecells - ref.posecells).max() < tol
+        b, rb = pcn(shape, precision=precision), P.PoseCellOracle(shape)
+        for x in (b, rb):
+            x.inject(1, loc)
+        with pytest.raises(ValueError):
+            b.run([[0.2, 0.01], [0.3, 0.0], [vt, 0.0], [0.2, 0.0]])
+        rb.update((0.2, 0.01))
+        rb.update((0.3, 0.0))
+        rb.excite_inhibit_normalise()
+        assert np.abs(b.posecells - rb.posecells).max() < tol
+    for vr in (np.nan, -np.inf):
+        net, ref = pcn(shape, precision=precision), P.PoseCellOracle(shape)
+        for x in (net, ref):
+            x.inject(1, loc)
+        assert net.update((0.3, vr)) == ref.update((0.3, vr)) == (0, 0, 0)
+        assert np.isnan(net.posecells).all() and np.isnan(ref.posecells).all()
+        assert net.get_pc_max() == (0, 0, 0)
+        assert [tuple(m) for m in net.run([[0.2, 0.0], [0.25, 0.3]])] == [(0, 0, 0)] * 2
+        assert np.isnan(net.posecells).all()

@@ -6,7 +6,9 @@ usage: python tools/pc_ab.py LIB.so[@ENV=V,...] [LIB2.so ...] [--shape 128,128,7
 (``@RS_PC_CTL=inline`` runs that library with the variable set)
 Each library runs in its own process (ctypes loads one copy), interleaved over
 rounds so clock drift hits every build alike: batched run() steps/s after a clock
-warm-up, and the state after the same odometry, compared across builds.
+warm-up, and the state after the same odometry, compared across builds.  A build
+whose state differs from the first one's by more than --tol (float32: the north_star
+1e-5) computed something else: its timing is not a valid A/B, and the tool exits 1.
 """
 import argparse
 import json
@@ -65,6 +67,8 @@ def main():
     ap.add_argument('--check', type=int, default=40)
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--precision', default='float32')
+    ap.add_argument('--tol', type=float, default=None,
+                    help='max |state difference| vs the first build (default 1e-5 float32, 1e-12 float64)')
     ap.add_argument('--child', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--out', default='')
     ap.add_argument('--mode', default='run', choices=('run', 'update', 'node'),
@@ -75,6 +79,8 @@ def main():
         child(a.libs[0], shape, a.steps, a.check, a.precision, a.out, a.mode)
         return
     import numpy as np
+    tol = a.tol if a.tol is not None else (1e-5 if a.precision == 'float32' else 1e-12)
+    bad = []
     res = {lib: [] for lib in a.libs}
     for rnd in range(a.rounds):
         for i, lib in enumerate(a.libs):
@@ -93,11 +99,17 @@ def main():
             if rnd == 0:
                 s0, s = np.load('/tmp/pc_ab_0.npy'), np.load(out)
                 r['max_abs_diff_vs_first'] = float(np.abs(s - s0).max())
+                if not r['max_abs_diff_vs_first'] <= tol:   # NaN fails too
+                    bad.append((lib, r['max_abs_diff_vs_first']))
                 print(json.dumps(r), flush=True)
     for lib in a.libs:
         v = sorted(res[lib])
         print(json.dumps({'lib': lib, 'us_per_step_min': v[0], 'us_per_step_median': v[len(v) // 2],
                           'all': [round(x, 2) for x in res[lib]]}), flush=True)
+    if bad:
+        print('pc_ab: INVALID A/B -- these builds end in a different state than %s (tol %g): %s'
+              % (a.libs[0], tol, bad), file=sys.stderr, flush=True)
+        raise SystemExit(1)
 
 
 if __name__ == '__main__':

@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
     }
     rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
     unsigned long long* dbg;
-    const size_t ndbg = 7 * 4096 * 8;
+    const size_t ndbg = 8 * 4096 * 8;
     CK(hipMalloc(&dbg, ndbg * 8));
     CK(hipMemset(dbg, 0, ndbg * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
@@ -103,10 +103,10 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
     const int nb = h->nPart;
-    static const char* kname[7] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
-                                   "excite_cols", "path_cols"};
-    static const int kns[7] = {4, 6, 5, 5, 0, 5, 5};
-    for (int kid = 0; kid < 7; ++kid) {
+    static const char* kname[8] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
+                                   "excite_cols", "path_cols", "halo"};
+    static const int kns[8] = {4, 6, 5, 5, 0, 5, 5, 7};
+    for (int kid = 0; kid < 8; ++kid) {
         if (kid == 4) continue;  // shader-clock stamps, below
         const int ns = kns[kid];
         if (st[(size_t)kid * 4096 * 8] == 0) continue;  // kernel not used by this step form
@@ -155,6 +155,33 @@ int main(int argc, char** argv) {
             }
             printf("   excite layer-5 %-28s median %6.0f cycles\n", nm[i - 1], median(c));
         }
+    }
+    if (h->halo) {  // back-to-back launch cost of the halo kernel alone, and of an empty one
+        hipEvent_t c0, c1;
+        CK(hipEventCreate(&c0));
+        CK(hipEventCreate(&c1));
+        const dim3 g(h->cgx * h->cgy), b(HF_NT);
+        const int reps = 500;
+        float t = 0;
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(empty_kernel, g, b, 0, h->stream, nullptr);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
+        PcCtlHalo c;
+        make_ctl_halo(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i)
+            hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, (float*)h->dQ,
+                               h->dPart, h->nPart, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
+                               (const float*)h->dFilt, h->nf, c, X, Y, h->cgx, h->kf);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("halo step alone: %.2f us/launch\n", 1e3 * t / reps);
+        rs_pc_destroy(h);
+        return 0;
     }
     if (h->streamed) {
         printf("stream tile BX=%d WR=%d KC=%d grid %d blocks\n", h->sbx, h->swr, h->sg.KC,
