@@ -141,11 +141,17 @@ constexpr int RES_SLOTS = 256;
 // still holding it after the stream has synchronised.
 constexpr unsigned long long RES_NONE = 0ull;
 // Step outputs are >= 0 or NaN (every step ends in a clamp), so the value bits order
-// like the values; every NaN is given one bit pattern above +inf, so that, as in numpy's
-// argmax, a NaN beats every number and the first NaN wins.
+// like the values (-0 taken as +0); every NaN is given one bit pattern above +inf, so
+// that, as in numpy's argmax, a NaN beats every number and the first NaN wins.
 __device__ inline unsigned long long argmax_key(float v, unsigned lin) {
-    const unsigned bits = v != v ? 0x7FC00000u : __float_as_uint(v);
+    const unsigned bits = v != v ? 0x7FC00000u : v == 0.f ? 0u : __float_as_uint(v);  // -0 as +0
     return ((unsigned long long)bits << 32) | (0xFFFFFFFFu - lin);
+}
+// The clamps P[P < 0] = 0 (posecell_network.py:300,314): as the reference, a NaN stays
+// a NaN (x > 0 ? x : 0 would zero it)
+template <typename T>
+__device__ inline T pc_clamp(T x) {
+    return x < T(0) ? T(0) : x;
 }
 // The same order for (value, index) pairs (float64 steps, get_pc_max): a NaN beats every
 // number, ties and NaNs among themselves go to the lower index; start from (-inf, ~0u).
@@ -160,6 +166,11 @@ __device__ inline bool pc_better(T v, unsigned l, T bv, unsigned bl) {
 #ifndef PC_STAMP
 #define PC_STAMP(kid, sid) \
     do {                   \
+    } while (0)
+#endif
+#ifndef PC_STAMPW
+#define PC_STAMPW(kid) \
+    do {               \
     } while (0)
 #endif
 
@@ -346,7 +357,7 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
         for (int x = 0; x < FL; ++x)
 #pragma unroll
             for (int y = 0; y < FL; ++y) acc += w[x * HY + y] * f[x * FL + y];
-        s_r[idx] = acc > T(0) ? acc : T(0);
+        s_r[idx] = pc_clamp(acc);
     }
     __syncthreads();
 
@@ -363,7 +374,7 @@ __global__ __launch_bounds__(NT) void pc_path_kernel(
             T acc = 0;
 #pragma unroll
             for (int z = 0; z < FL; ++z) acc += s_r[idx + z * BX * BY] * s_zf[z];
-            T v = acc > T(0) ? acc : T(0);
+            T v = pc_clamp(acc);
             v = nrm(v);
             P[((size_t)gk * X + gi) * Y + gj] = v;
             const unsigned lin = ((unsigned)gi * Y + gj) * TH + gk;
@@ -708,7 +719,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 }
             }
 #pragma unroll
-            for (int i = 0; i < BX; ++i) s_r[(kk * BX + i) * YP + j] = acc[i] > T(0) ? acc[i] : T(0);
+            for (int i = 0; i < BX; ++i) s_r[(kk * BX + i) * YP + j] = pc_clamp(acc[i]);
         }
     }
     // normalisation total (its loads were issued at entry): per thread, then per
@@ -742,7 +753,7 @@ __global__ __launch_bounds__(RT_NT) void pc_path_rows(
                 T acc = 0;
 #pragma unroll
                 for (int z = 0; z < FL; ++z) acc += s_r[((kq + z) * BX + i) * YP + j] * (T)ctl_zf(ctl, z);
-                T val = acc > T(0) ? acc : T(0);
+                T val = pc_clamp(acc);
                 val = nrm(val);
                 st_wt(&P[((size_t)gk * X + gi) * Y + j], val);
                 const unsigned lin = ((unsigned)gi * Y + j) * TH + gk;
@@ -1143,7 +1154,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
                 }
             }
 #pragma unroll
-            for (int i = 0; i < BX; ++i) ring[s][i] = acc[i] > T(0) ? acc[i] : T(0);
+            for (int i = 0; i < BX; ++i) ring[s][i] = pc_clamp(acc[i]);
             if (it >= 2 * HALF) {
                 const int o = it - 2 * HALF, gk = k0 + o;
 #pragma unroll
@@ -1151,7 +1162,7 @@ __global__ __launch_bounds__(64 * WR * WC) PC_ST_WAVES void pc_path_stream(
                     T v = 0;
 #pragma unroll
                     for (int z = 0; z < FL; ++z) v += ring[(s + 1 + z) % FL][i] * zf[z];
-                    v = v > T(0) ? v : T(0);
+                    v = pc_clamp(v);
                     v = nrm(v);
                     s_out[(o * BXB + rg * BX + i) * YT + col] = v;
                     const int gi = i0 + rg * BX + i;
@@ -1856,7 +1867,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         for (int i = 0; i < TXH; ++i)
 #pragma unroll
             for (int c = 0; c < CP; ++c) {
-                const T v = acc[i][c] > T(0) ? acc[i][c] : T(0);
+                const T v = pc_clamp(acc[i][c]);
                 T* sp = s_p + ((hf * TXH + i) * TY + c0 + c) * PP + SPO;
                 sp[L] = v;
                 if (Lw1 != INT_MIN) sp[Lw1] = v;
@@ -1903,7 +1914,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                 T x = 0;
 #pragma unroll
                 for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
-                x = x > T(0) ? x : T(0);
+                x = pc_clamp(x);
                 x = nrm(x);
                 v[o] = x;
             }
@@ -2008,10 +2019,15 @@ constexpr int HF_Q = HF_T + 2 * HALF;         // 10: a layer's excited (Q) windo
 constexpr int HF_NW = 9, HF_NT = 64 * HF_NW;  // 576 threads: one task per (layer, window row) at TH = 36
 constexpr int HF_TH = 36;                     // the theta extent instantiated (configs[1], the ROS node)
 constexpr int HF_UMAX = 22 * 22;              // union cells staged by LDS-DMA (|shifts| spread <= 6)
-constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;  // theta-pass window rows: pitch 18 (the y pass's 8-byte row reads are conflict-free)
+// theta-pass windows, (e, i) pairs [j][rx][ry], row pitch 18 pairs: the y pass's 16-byte
+// row reads (16 lanes on consecutive rows, 36 dwords apart) are conflict-free
+constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;
 constexpr int HF_YJ = HF_W * HF_Q + 10;       // y-pass outputs per layer (pitch: the x pass reads conflict-free)
 constexpr int HF_QJ = HF_Q * HF_Q + 4;        // Q window per layer
 constexpr int HF_EXP_MAX = 64;                // steps whose keys pc_halo_finish exports itself
+#ifndef HF_YX_DPP
+#define HF_YX_DPP 0  // 1: y and x passes fused by DPP row shifts (measured slower: 1.56 + 1.20 vs 0.92 + 1.04 us)
+#endif
 
 // One step's control, a kernel argument (formed on the host by make_ctl_halo).
 struct PcCtlHalo {
@@ -2023,6 +2039,11 @@ struct PcCtlHalo {
     int wrap;                    // the union is a whole period in x or y (windows wrap inside it)
 };
 typedef float hf_f2 __attribute__((ext_vector_type(2)));  // (excitatory, inhibitory) pairs: packed FMAs
+// lane l + A's value within each 16-lane row (DPP row_shl:A; 0 past the row's end)
+template <int A>
+__device__ inline float hf_row_shl(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x100 + A, 0xF, 0xF, true));
+}
 
 // The normalisation total of a step from its per-block partials, formed by every wave
 // itself in one fixed order (so every block gets the same bits): 4 per lane, then DPP.
@@ -2053,7 +2074,9 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     constexpr int BBUF = WBUF > YBUF ? WBUF : YBUF;
     constexpr int PP = TH + 64;   // path outputs per cell: rows TH dwords apart modulo the 64 banks
     static_assert(HF_T * HF_T * PP <= BBUF && TH * HF_QJ <= 2 * TH * HF_WJ, "buffer reuse");
-    __shared__ __attribute__((aligned(16))) float s_t[2 * TH * HF_WJ];  // theta pass e | i; then Q
+    // theta-pass (e, i) windows, then a dump slot per thread (a lane outside a layer's
+    // window stores there: no branch); then Q
+    __shared__ __attribute__((aligned(16))) float s_t[2 * (TH * HF_WJ + HF_NT)];
     __shared__ __attribute__((aligned(16))) float s_b[BBUF];  // union image; then y pass e | i; then path outputs
     __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_fo[TH];
@@ -2101,6 +2124,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     }
     // the normalisation of the state entering the step, the filter table, the control
+    // (lane L of every wave holds layer L's window start, read by readlane in phase 2)
+    const int lsx = ctl.sx[lane < TH ? lane : 0], lsy = ctl.sy[lane < TH ? lane : 0];
     const float fr = tid < nf * FT ? filt[tid] : 0.f;
     static_assert(RT_NFMAX * FT <= HF_NT, "one filter tap per thread");
     if (tid < TH) s_fo[tid] = ctl.fo[tid] * ST_FTP;
@@ -2112,80 +2137,192 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     co_lds_barrier();
     PC_STAMP(7, 1);
 
-    // 2. per union cell: its column, scaled (the argmax of the state entering the step,
-    //    own tile), the theta pass of both Gaussians as packed (e, i) FMAs, stored for
-    //    every layer window holding the cell.  Windows are [j][rx][ry] with row pitch
-    //    HF_WP, so a cell's place in layer j's window, j*HF_WJ + (ui-sx_j)*HF_WP + vi-sy_j,
-    //    is the cell's own offset plus a per-layer scalar (no per-layer address math);
-    //    only a union spanning a whole period (wrap) needs the modular form.
-    float* s_te = s_t;
-    float* s_ti = s_t + TH * HF_WJ;
+    // 2. the theta pass of both Gaussians, as packed (e, i) FMAs, into the layers'
+    //    windows [j][rx][ry] (row pitch HF_WP).
+    hf_f2* s_tw = reinterpret_cast<hf_f2*>(s_t);
     unsigned long long bk = 0ull;
     const bool want_key = slot_prev != nullptr;
     hf_f2 gei[FL];
 #pragma unroll
     for (int t = 0; t < FL; ++t) gei[t] = hf_f2{k.ge[t], k.gi[t]};
-    // one union cell c: FAST = the column from the LDS-DMA image and no wrap (the
-    // common case: straight-line code, one cell per thread); otherwise the column from
-    // memory or the windows wrapping inside a whole-period union
-    auto cell_pass = [&](int c, auto fast_c, auto wrap_c) __attribute__((always_inline)) {
-        constexpr bool FAST = decltype(fast_c)::value, WRAP = decltype(wrap_c)::value;
-        const int ui = c / UH, vi = c - ui * UH;
-        int gr = ux0 + ui, gc = uy0 + vi;
-        gr -= gr >= X ? X : 0;
-        gc -= gc >= Y ? Y : 0;
-        float p[TH];
-        const co_f4* src = FAST || dma ? reinterpret_cast<const co_f4*>(s_b + c * TH)
-                                       : reinterpret_cast<const co_f4*>(U + ((size_t)gr * Y + gc) * TH);
+    PC_STAMP(4, 0);
+    if (dma && !ctl.wrap) {
+        // the common case, read straight from the union image [cell][layer]: wave w < 8
+        // takes window rows 4(w&3) .. +3 (a lane per window cell) through the layers
+        // [18(w>>2), +18).  Layer j's window cell (rx, ry) is union cell (rx + sx_j,
+        // ry + sy_j); its 7 theta taps are 7 consecutive floats of that cell's column,
+        // held as 16-byte quads of the column in registers (conflict-free reads: lanes
+        // 144 bytes apart).  While the shift stays the layer before's, a layer needs at
+        // most one new quad, read PF layers ahead; a layer with a new shift (a
+        // wave-uniform branch, a few per run) reloads the quads its taps and the next
+        // PF layers' reach.  Each quad is scaled by 1/t as it arrives (the same products
+        // as every other form's); every lane's store is one of a window's own cells.
+        if (nrm.div) {   // 1/t not finite (t tiny): divide the image in place first
+            for (int c = tid; c < nu; c += HF_NT) {
+                co_f4* col = reinterpret_cast<co_f4*>(s_b + c * TH);
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const co_f4 x = src[v];
+                for (int v = 0; v < NV; ++v) {
+                    co_f4 x = col[v];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
-        }
-        nrm(p);
-        if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
-            const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
-#pragma unroll
-            for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
-        }
-        // the cell's own offset, opaque to the compiler: each layer's window place is
-        // then one add of a scalar, not a re-derived product
-        int cb = ui * HF_WP + vi;
-        asm volatile("" : "+v"(cb));
-#pragma unroll
-        for (int j = 0; j < TH; ++j) {
-            const int sxj = ctl.sx[j], syj = ctl.sy[j];
-            int a;
-            bool in;
-            if constexpr (WRAP) {
-                int rx = ui - sxj, ry = vi - syj;
-                rx += rx < 0 ? UW : 0;
-                ry += ry < 0 ? UH : 0;
-                in = (unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W;
-                a = j * HF_WJ + rx * HF_WP + ry;
-            } else {
-                in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
-                a = cb + __builtin_amdgcn_readfirstlane(j * HF_WJ - sxj * HF_WP - syj);
+                    for (int w = 0; w < 4; ++w) x[w] = nrm(x[w]);
+                    col[v] = x;
+                }
             }
-            if (in) {
+            co_lds_barrier();
+        }
+        if (wave < 8) {
+            constexpr int JH = TH / 2, PF = 3;
+            const int rx = 4 * (wave & 3) + (lane >> 4), ry = lane & 15;
+            const int loff = (lsx * UH + lsy) * TH;   // lane L: layer L's window place in the union
+            const int cbase = (rx * UH + ry) * TH;
+            auto run = [&](auto hh) __attribute__((always_inline)) {
+                constexpr int J0 = decltype(hh)::value * JH;
+                // quads kq = 0 .. NQ-1 hold layers 4 (QB + kq) .. +3 (mod TH) of the current cell
+                constexpr int QB = (J0 - HALF + 4 * TH) / 4 - TH, NQ = (J0 + JH - 1 + HALF - 4 * QB) / 4 + 1;
+                co_f4 qd[NQ];
+                hf_f2* dst = s_tw + J0 * HF_WJ + (rx * HF_WP + ry);
+                int prev = __builtin_amdgcn_readlane(loff, J0);
+                const float* col = s_b + cbase + prev;
+                auto ld = [&](int kq) {
+                    qd[kq] = *reinterpret_cast<const co_f4*>(col + ((4 * (QB + kq) + 4 * TH) % TH)) * nrm.r;
+                };
+                // quads holding layers lo .. hi (relative to 4 QB), clipped to the run
+                auto ld_span = [&](int lo, int hi) __attribute__((always_inline)) {
+#pragma unroll
+                    for (int kq = 0; kq < NQ; ++kq)
+                        if (4 * kq + 3 >= lo && 4 * kq <= hi) ld(kq);
+                };
+                ld_span(J0 - HALF - 4 * QB, J0 + HALF + PF - 4 * QB);
+                auto tapv = [&](int e) { return qd[e / 4][e % 4]; };
+                // layer jj's taps (first tap e0 relative to 4 QB) in the reference's order
+                auto one = [&](int jj) __attribute__((always_inline)) {
+                    const int e0 = J0 + jj - HALF - 4 * QB;
+                    hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+                    for (int t = 0; t < FL; ++t) eg += gei[t] * tapv(e0 + t);
+                    dst[jj * HF_WJ] = eg;
+                };
+                // the new shift of layer jj, if any; else the quad its taps reach PF layers on
+                auto enter = [&](int jj, int o) __attribute__((always_inline)) {
+                    const int e0 = J0 + jj - HALF - 4 * QB;
+                    if (o == prev) {
+                        const int e = e0 + 2 * HALF + PF;
+                        if (e % 4 == 0 && e / 4 < NQ) ld(e / 4);
+                    } else {
+                        prev = o;
+                        col = s_b + cbase + o;
+                        ld_span(e0, e0 + 2 * HALF + PF);
+                    }
+                };
+                // layers in pairs: two independent FMA chains interleaved, unless the
+                // second layer of the pair takes a new shift (then one after the other,
+                // the first before its quads are replaced)
+                static_assert(JH % 2 == 0, "layer pairs");
+#pragma unroll
+                for (int jj = 0; jj < JH; jj += 2) {
+                    if (jj > 0) enter(jj, __builtin_amdgcn_readlane(loff, J0 + jj));
+                    const int o1 = __builtin_amdgcn_readlane(loff, J0 + jj + 1);
+                    if (o1 == prev) {
+                        enter(jj + 1, o1);
+                        const int e0 = J0 + jj - HALF - 4 * QB;
+                        hf_f2 ea = {0.f, 0.f}, eb = {0.f, 0.f};
+#pragma unroll
+                        for (int t = 0; t < FL; ++t) {
+                            ea += gei[t] * tapv(e0 + t);
+                            eb += gei[t] * tapv(e0 + 1 + t);
+                        }
+                        dst[jj * HF_WJ] = ea;
+                        dst[(jj + 1) * HF_WJ] = eb;
+                    } else {
+                        one(jj);
+                        enter(jj + 1, o1);
+                        one(jj + 1);
+                    }
+                }
+            };
+            if (wave < 4) run(std::integral_constant<int, 0>{});
+            else run(std::integral_constant<int, 1>{});
+        } else if (want_key) {
+            // wave 8: the argmax of the state entering the step over the own tile (lane:
+            // cell lane & 15, quads lane >> 4 + 4 m)
+            const int i = (lane & 15) >> 2, jc = lane & 3;
+            int cu = co_wrap(2 * HALF - ctl.ux, X) + i, cv = co_wrap(2 * HALF - ctl.uy, Y) + jc;
+            cu -= cu >= X ? X : 0;
+            cv -= cv >= Y ? Y : 0;
+            if (i < tw && jc < tht && cu < UW && cv < UH) {
+                const unsigned lin0 = ((unsigned)(x0 + i) * Y + (y0 + jc)) * TH;
+                const co_f4* src = reinterpret_cast<const co_f4*>(s_b + (cu * UH + cv) * TH);
+                for (int v = lane >> 4; v < NV; v += 4) {
+                    const co_f4 x = src[v];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) bk = max(bk, argmax_key(x[w] * nrm.r, lin0 + 4 * v + w));  // (r = 1 once divided)
+                }
+            }
+        }
+    } else {
+        // a union spanning a whole period (the windows wrap inside it), or one larger
+        // than the LDS-DMA image (columns from memory): thread c takes union cell c's
+        // column, scales it, forms all TH theta-pass outputs in registers and stores
+        // those of the windows holding the cell (a lane outside a window stores into its
+        // own dump slot, so the layers' chains interleave with no exec changes)
+        auto cell_pass = [&](int c, auto wrap_c) __attribute__((always_inline)) {
+            constexpr bool WRAP = decltype(wrap_c)::value;
+            const int ui = c / UH, vi = c - ui * UH;
+            int gr = ux0 + ui, gc = uy0 + vi;
+            gr -= gr >= X ? X : 0;
+            gc -= gc >= Y ? Y : 0;
+            float p[TH];
+            if (dma) {
+                const co_f4* src = reinterpret_cast<const co_f4*>(s_b + c * TH);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const co_f4 x = src[v];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
+                }
+            } else {
+                const co_f4* src = reinterpret_cast<const co_f4*>(U + ((size_t)gr * Y + gc) * TH);
+#pragma unroll
+                for (int v = 0; v < NV; ++v) {
+                    const co_f4 x = src[v];
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
+                }
+            }
+            nrm(p);
+            if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
+                const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
+#pragma unroll
+                for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
+            }
+#pragma unroll
+            for (int j = 0; j < TH; ++j) {
+                const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
                 hf_f2 eg = {0.f, 0.f};
 #pragma unroll
                 for (int t = 0; t < FL; ++t) eg += gei[t] * p[(j + t + TH - HALF) % TH];
-                s_te[a] = eg.x;
-                s_ti[a] = eg.y;
+                if constexpr (WRAP) {
+                    int rx = ui - sxj, ry = vi - syj;
+                    rx += rx < 0 ? UW : 0;
+                    ry += ry < 0 ? UH : 0;
+                    if ((unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W)
+                        s_tw[j * HF_WJ + rx * HF_WP + ry] = eg;
+                } else {
+                    const bool in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
+                    s_tw[in ? j * HF_WJ + (ui - sxj) * HF_WP + (vi - syj) : TH * HF_WJ + tid] = eg;
+                }
             }
+        };
+        if (ctl.wrap) {
+#pragma unroll 1
+            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::true_type{});
+        } else {
+#pragma unroll 1
+            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{});
         }
-    };
-    if (dma && !ctl.wrap) {
-        if (tid < nu) cell_pass(tid, std::true_type{}, std::false_type{});
-    } else if (ctl.wrap) {
-#pragma unroll 1
-        for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{}, std::true_type{});
-    } else {
-#pragma unroll 1
-        for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{}, std::false_type{});
     }
+    PC_STAMP(4, 1);
+    PC_STAMPW(5);
     if (want_key && tid < tw * tht) {
         // an own cell outside the union (a large uniform shift): its key from memory
         const int i = tid / tht, j = tid - i * tht;
@@ -2206,19 +2343,79 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     co_lds_barrier();
     PC_STAMP(7, 2);
 
+#if HF_YX_DPP
+    // 3+4. y and x passes fused, one 16-lane DPP row per layer (4 layers per wave, 36
+    //    layers = 9 waves): lane rx of layer j's row forms its window row's y pass (10
+    //    outputs of each Gaussian) in registers; the x pass then takes rows rx .. rx+6
+    //    from the row's next lanes by DPP row_shl (which never leaves the 16-lane row),
+    //    so Q row qa = rx (lanes rx < 10) is formed with no LDS round trip or barrier
+    //    between the passes; the inhibition (:339-340) and the partial sum over the
+    //    layer's shifted own tile (Q rows / columns 3 .. 3+tw) follow.  Q goes to the
+    //    (dead) union image.
+    float* s_q = s_b;
+    double qs = 0.0;
+    {
+        static_assert(HF_NW * 4 == TH && HF_W == 16, "one DPP row of 16 lanes per layer");
+        const int j = wave * 4 + (lane >> 4), rx = lane & 15;
+        const co_f4* rw = reinterpret_cast<const co_f4*>(s_tw + j * HF_WJ + rx * HF_WP);
+        hf_f2 w[HF_W];   // (e, i) of the row's 16 cells
+#pragma unroll
+        for (int q = 0; q < HF_W / 2; ++q) {
+            const co_f4 a = rw[q];
+            w[2 * q] = hf_f2{a.x, a.y};
+            w[2 * q + 1] = hf_f2{a.z, a.w};
+        }
+        float ye[HF_Q], yi[HF_Q];
+#pragma unroll
+        for (int c = 0; c < HF_Q; ++c) {
+            hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+            for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[c + t2];
+            ye[c] = eg.x;
+            yi[c] = eg.y;
+        }
+        const bool orow = (unsigned)(rx - HALF) < (unsigned)tw;
+#pragma unroll
+        for (int qc = 0; qc < HF_Q; ++qc) {
+            // rows rx .. rx + 6 of the same layer (lanes past the row's end read 0)
+            const float de[FL] = {ye[qc], hf_row_shl<1>(ye[qc]), hf_row_shl<2>(ye[qc]), hf_row_shl<3>(ye[qc]),
+                                  hf_row_shl<4>(ye[qc]), hf_row_shl<5>(ye[qc]), hf_row_shl<6>(ye[qc])};
+            const float di[FL] = {yi[qc], hf_row_shl<1>(yi[qc]), hf_row_shl<2>(yi[qc]), hf_row_shl<3>(yi[qc]),
+                                  hf_row_shl<4>(yi[qc]), hf_row_shl<5>(yi[qc]), hf_row_shl<6>(yi[qc])};
+            float e = 0.f, g = 0.f;
+#pragma unroll
+            for (int a = 0; a < FL; ++a) {
+                e += k.ge[a] * de[a];
+                g += k.gi[a] * di[a];
+            }
+            const float v = (e - g) * k.scale;
+            const float q = (v < k.inhib) ? 0.f : v - k.inhib;
+            if (rx < HF_Q) {
+                const bool own = orow && (unsigned)(qc - HALF) < (unsigned)tht;
+                if (own) qs += (double)q;
+                if constexpr (EXC) {
+                    if (own) Uo[((size_t)(x0 + rx - HALF) * Y + (y0 + qc - HALF)) * TH + j] = q;
+                } else {
+                    s_q[j * HF_QJ + rx * HF_Q + qc] = q;
+                }
+            }
+        }
+    }
+    PC_STAMP(7, 3);
+    float* s_po = s_t;   // the path outputs, into the (dead) theta-pass windows
+#else
     // 3. y pass: task (layer j, window row rx) -> 10 outputs of each Gaussian
     float* s_ye = s_b;
     float* s_yi = s_b + TH * HF_YJ;
     for (int t = tid; t < TH * HF_W; t += HF_NT) {
         const int j = t >> 4, rx = t & 15;
-        const hf_f2* re = reinterpret_cast<const hf_f2*>(s_te + j * HF_WJ + rx * HF_WP);
-        const hf_f2* ri = reinterpret_cast<const hf_f2*>(s_ti + j * HF_WJ + rx * HF_WP);
+        const co_f4* rw = reinterpret_cast<const co_f4*>(s_tw + j * HF_WJ + rx * HF_WP);
         hf_f2 w[HF_W];   // (e, i) of the row's 16 cells
 #pragma unroll
         for (int q = 0; q < HF_W / 2; ++q) {
-            const hf_f2 a = re[q], b = ri[q];
-            w[2 * q] = hf_f2{a.x, b.x};
-            w[2 * q + 1] = hf_f2{a.y, b.y};
+            const co_f4 a = rw[q];
+            w[2 * q] = hf_f2{a.x, a.y};
+            w[2 * q + 1] = hf_f2{a.z, a.w};
         }
         hf_f2* de = reinterpret_cast<hf_f2*>(s_ye + j * HF_YJ + rx * HF_Q);
         hf_f2* di = reinterpret_cast<hf_f2*>(s_yi + j * HF_YJ + rx * HF_Q);
@@ -2267,6 +2464,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
         }
     }
+    float* s_po = s_b;
+#endif
     if constexpr (!EXC) {
         co_lds_barrier();
         PC_STAMP(7, 4);
@@ -2274,7 +2473,6 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         //    row pair ap) -> 2 outputs from 8 x 7 Q values; into [cell][3 + j] rows with
         //    wrapped copies (layers TH-3.. before, 0..6 after), so every theta window
         //    below is one contiguous aligned run
-        float* s_po = s_b;
         for (int t = tid; t < TH * 8; t += HF_NT) {
             const int j = t >> 3, tb = t & 3, ap = (t >> 2) & 1;
             float f[FT];
@@ -2295,7 +2493,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                     for (int y = 0; y < FL; ++y) a1 += w[y] * f[(r - 1) * FL + y];
                 }
             }
-            const float v0 = a0 > 0.f ? a0 : 0.f, v1 = a1 > 0.f ? a1 : 0.f;
+            const float v0 = pc_clamp(a0), v1 = pc_clamp(a1);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const float v = h ? v1 : v0;
@@ -2328,7 +2526,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 float x = 0.f;
 #pragma unroll
                 for (int z = 0; z < FL; ++z) x += r[o + z] * ctl.zf[z];
-                v[o] = x > 0.f ? x : 0.f;
+                v[o] = pc_clamp(x);
             }
             co_put(Uo, ((size_t)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g, v, wt, nbytes);
         }

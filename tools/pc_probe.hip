@@ -21,6 +21,14 @@ __device__ unsigned long long* pc_dbg;
             pc_dbg[((kid) * 4096 + b_) * 8 + (sid)] = __builtin_amdgcn_s_memrealtime(); \
         }                                                                               \
     } while (0)
+// per-wave stamp: wave w of the block at (kid + w / 8, w % 8)
+#define PC_STAMPW(kid)                                                                        \
+    do {                                                                                      \
+        if ((threadIdx.x & 63) == 0) {                                                        \
+            const unsigned b_ = blockIdx.y * gridDim.x + blockIdx.x, w_ = threadIdx.x >> 6;   \
+            pc_dbg[((kid + w_ / 8) * 4096 + b_) * 8 + w_ % 8] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                     \
+    } while (0)
 #include "posecell.hip"
 
 #define CK(x)                                                                  \
@@ -144,7 +152,26 @@ int main(int argc, char** argv) {
         printf("boundary %s -> %s: %.2f us (excite first start -> path last end %.2f us)\n", kname[ek],
                kname[pk], ((double)p0 - (double)e1) * 1e-2, ((double)p1 - (double)e0) * 1e-2);
     }
-    if (st[(size_t)4 * 4096 * 8] != 0) {  // shader-clock phases of layer 5 (excite stream)
+    if (h->halo && st[(size_t)4 * 4096 * 8] != 0) {  // the halo kernel's theta pass (stamps 4, 0..1)
+        std::vector<double> a, b;
+        for (int bb = 0; bb < h->nPart; ++bb) {
+            const unsigned long long* r4 = &st[((size_t)4 * 4096 + bb) * 8];
+            const unsigned long long* r7 = &st[((size_t)7 * 4096 + bb) * 8];
+            a.push_back((double)(r4[0] - r7[1]) * 10.0);
+            b.push_back((double)(r4[1] - r4[0]) * 10.0);
+        }
+        printf("   halo phase 2: barrier end -> task loop %.2f us, task loop %.2f us (wave 0, median)\n",
+               median(a) * 1e-3, median(b) * 1e-3);
+        printf("   halo phase 2 per wave, task loop end after phase 1 (median us):");
+        for (int w = 0; w < 9; ++w) {
+            std::vector<double> c;
+            for (int bb = 0; bb < h->nPart; ++bb)
+                c.push_back((double)(st[((size_t)(5 + w / 8) * 4096 + bb) * 8 + w % 8] -
+                                     st[((size_t)7 * 4096 + bb) * 8 + 1]) * 10.0);
+            printf(" %.2f", median(c) * 1e-3);
+        }
+        printf("\n");
+    } else if (st[(size_t)4 * 4096 * 8] != 0) {  // shader-clock phases of layer 5 (excite stream)
         const char* nm[6] = {"vmcnt wait", "lds store+prefetch+barrier", "y pass", "barrier 2",
                              "x pass", "theta pass"};
         for (int i = 1; i < 7; ++i) {
