@@ -355,7 +355,11 @@ def test_step_forms_agree_with_oracle(pcn, monkeypatch, precision, tol):
 
 def test_default_form_by_grid_size(pcn, monkeypatch):
     monkeypatch.delenv('RS_PC_FORM', raising=False)
-    assert pcn((64, 64, 36)).step_form() == 'rows'
+    assert pcn((64, 64, 36)).step_form() == 'halo'       # float32, TH = 36, <= 256 tiles
+    assert pcn((21, 21, 36)).step_form() == 'halo'
+    assert pcn((64, 64, 36), precision='float64').step_form() == 'rows'
+    assert pcn((68, 64, 36)).step_form() == 'rows'       # 17 x 16 tiles: more than one per CU
+    assert pcn((32, 32, 18)).step_form() == 'rows'       # TH != 36
     assert pcn((128, 128, 72)).step_form() == 'cols'
     assert pcn((128, 130, 72)).step_form() == 'stream'    # Y not a multiple of 4: no cols
     assert pcn((128, 128, 100)).step_form() == 'cols'     # theta extent beyond one block: chunked

@@ -1,12 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-L=pyratslam_amd/libratslam_hip.so
-ls $L > /dev/null || exit 1
-for m in run update node; do
-  echo "== mode $m 64"
-  timeout -k 10 200 python -u tools/pc_ab.py $L@RS_PC_FORM=rows $L@RS_PC_FORM=halo --shape 64,64,36 --rounds 3 --steps 3000 --mode $m > gpurun_out/ab_$m.log 2>&1 || { tail -20 gpurun_out/ab_$m.log; exit 1; }
-  tail -4 gpurun_out/ab_$m.log
-done
-echo "== 21"
-timeout -k 10 200 python -u tools/pc_ab.py $L@RS_PC_FORM=rows $L@RS_PC_FORM=halo --shape 21,21,36 --rounds 3 --steps 3000 > gpurun_out/ab_21.log 2>&1 || { tail -20 gpurun_out/ab_21.log; exit 1; }
-tail -4 gpurun_out/ab_21.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gputest_r4_v1.log 2>&1 || { tail -40 gpurun_out/gputest_r4_v1.log; exit 1; }
+tail -3 gpurun_out/gputest_r4_v1.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
