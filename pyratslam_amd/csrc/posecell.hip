@@ -2509,9 +2509,11 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         //    16-byte write-through store of U (normalised by the next launch)
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(float), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(float) <= (size_t)INT_MAX;
-        for (int t = tid; t < HF_T * HF_T * NV; t += HF_NT) {
+        static_assert(HF_T * HF_T * NV <= HF_NT, "one theta-filter task per thread");
+        if (tid < HF_T * HF_T * NV) {
+            const int t = tid;
             const int cell = t / NV, g = t - cell * NV, ta = cell >> 2, tb = cell & 3;
-            if (ta >= tw || tb >= tht) continue;
+            if (ta < tw && tb < tht) {
             const co_f4* sv = reinterpret_cast<const co_f4*>(s_po + cell * PP + 4 * g);
             float r[12];
 #pragma unroll
@@ -2528,7 +2530,9 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 for (int z = 0; z < FL; ++z) x += r[o + z] * ctl.zf[z];
                 v[o] = pc_clamp(x);
             }
-            co_put(Uo, ((size_t)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g, v, wt, nbytes);
+            const unsigned lin = ((unsigned)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g;
+            co_put(Uo, lin, v, wt, nbytes);
+            }
         }
     }
     // the block's partial sum and argmax key
@@ -2540,10 +2544,10 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     }
     co_lds_barrier();
     if (tid == 0) {
-        double s = 0.0;
+        double bsum = 0.0;
 #pragma unroll
-        for (int w = 0; w < HF_NW; ++w) s += s_red[w];
-        st_wt(&part_out[blockIdx.x], s);
+        for (int w = 0; w < HF_NW; ++w) bsum += s_red[w];
+        st_wt(&part_out[blockIdx.x], bsum);
         if (want_key) {
             for (int w = 1; w < HF_NW; ++w) bk = max(bk, s_bk[w]);
             atomicMax(slot_prev + (blockIdx.x & (RES_SLOTS - 1)), bk);
@@ -2590,7 +2594,7 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     __syncthreads();
     if (tid == 0) {
         bk = max(max(s_bk[0], s_bk[1]), max(s_bk[2], s_bk[3]));
-        atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
+        if (slot) atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
         s_last = 0;
         if (nexp > 0) {
             // the key has reached memory (agent-scope atomics execute there) before
@@ -3030,9 +3034,17 @@ void make_ctl_halo(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, 
     c->wrap = HF_W + mxx - mnx > h->X || HF_W + mxy - mny > h->Y;
 }
 
-// n steps of the halo form: n dependent launches (the state ping-pongs between P and Q,
-// the partial sums between the two halves of dPart), then pc_halo_finish (normalised
-// state, last step's argmax, every step's key to the host), one host sync.
+// n steps of the halo form: one launch each (step s reads the state in one buffer,
+// scaled by the partials of the step before, and writes U into the other; the partial
+// sums ping-pong between the two halves of dPart), then pc_halo_finish: the state
+// normalised back into dP, the last step keyed, every step's key exported to the host
+// (its last block, by a counter), the float64 volume for an eager readback; one host
+// sync.  (An update() that ended in its own launch -- its last block keying the new
+// state from per-block records, the state left unnormalised until the next load --
+// measured slower than this second launch: 27.5 vs 26.3 us per call at 64x64x36, the
+// records' drain, the counter atomic and the records' loads being memory round trips in
+// series; with the records stored straight into host memory the host's wait grew to
+// 28.9 us for a 13.4 us call.)
 int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                 const double* zf, int32_t* out_xyz) {
     RS_TRY(pc_grow_steps(h, n));

@@ -248,3 +248,57 @@ def test_state_roundtrip_inject_argmax_total(halo):
     from pyratslam_amd import _lib
     _lib.check(net._lib.rs_pc_read(net._h, _lib.ptr(buf, ctypes.c_double)))
     assert buf[3, 4, 5] == pytest.approx(back[3, 4, 5] + 5.0, rel=1e-6)
+
+
+def test_entry_points_between_updates(halo):
+    """inject, get_pc_max, total, the volume read, write and the next update() between
+    update() calls see the normalised state the reference's update() leaves."""
+    shape = (64, 64, 36)
+    od = odometry(6, 8)
+    net = halo(shape)
+    ref = P.PoseCellOracle(shape)
+    for x in (net, ref):
+        x.inject(1, (20, 40, 7))
+    for v in od[:2]:
+        assert net.update(v) == ref.update(v)
+    net.inject(0.3, (50, 10, 30))                 # inject into a pending state
+    ref.inject(0.3, (50, 10, 30))
+    assert net.get_pc_max() == ref.get_pc_max()
+    assert abs(net.total() - ref.posecells.sum()) < 1e-4
+    for v in od[2:4]:
+        assert net.update(v) == ref.update(v)
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+    v0 = ref.posecells.copy()
+    assert net.update(od[4]) == ref.update(od[4])
+    net.posecells = v0                            # a write replaces the pending volume
+    ref.posecells = v0.copy()
+    assert net.update(od[5]) == ref.update(od[5])
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+
+
+@pytest.mark.parametrize('case', ['six_layers', 'twins'])
+def test_argmax_exact_ties(halo, case):
+    """Exact ties in the new state: six identical packets 6 layers apart in one cell
+    (without translation the step keeps the 6-fold symmetry: six tied cells in one tile)
+    and two identical packets 32 cells apart (ties across blocks); the lowest index
+    wins, as numpy's argmax, per call and batched, against the C oracle."""
+    from oracle import c_oracle as C
+    shape = (64, 64, 36)
+    v = np.zeros(shape)
+    if case == 'six_layers':
+        v[10, 20, 0::6] = 1.0
+        od = [(0.0, 0.0), (0.0, 0.1), (0.0, 0.0)]
+    else:
+        v[10, 20, 5] = v[42, 20, 5] = 1.0
+        od = [(0.0, 0.0), (0.4, 0.0), (0.4, 0.0), (0.2, 0.1)]
+    ref = C.PoseCellC(shape)
+    ref.posecells = v.copy()
+    want = [ref.update(o) for o in od]
+    for batched in (False, True):
+        net = halo(shape)
+        net.posecells = v
+        got = [tuple(r) for r in net.run(od)] if batched else [net.update(o) for o in od]
+        assert got == want, (case, batched, got, want)
+        own, p = own_argmax(net)
+        assert own == want[-1]
+        assert np.abs(p - ref.posecells).max() < F32_TOL

@@ -64,6 +64,8 @@ def main():
         if p.returncode != 0:
             print(p.stderr[-3000:], file=sys.stderr)
             raise SystemExit(p.returncode)
+        if p.stderr.strip():
+            print(p.stderr.strip()[-600:], file=sys.stderr, flush=True)
         print(p.stdout.strip().splitlines()[-1], flush=True)
 
 

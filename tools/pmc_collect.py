@@ -25,7 +25,7 @@ import re
 import shutil
 
 SCANS = {'headline': (1000, 10240), 'stress': (10000, 5120), 'library': (100000, 2048)}
-PCS = {'pc64': ('rows', [64, 64, 36]), 'pc128': ('cols', [128, 128, 72])}
+PCS = {'pc64': ('halo', [64, 64, 36]), 'pc128': ('cols', [128, 128, 72])}
 
 
 def short(name):
@@ -120,6 +120,26 @@ def traffic_of(configs, tag):
                 'hbm_bytes_per_launch': e.get('hbm_bytes_per_dispatch'),
                 'wave_cycle_split': e.get('wave_cycle_split'),
                 'source': f'{tag}_pmc_summary.json'}
+        elif c in PCS and PCS[c][0] == 'halo':
+            # one launch per step; the finishing kernel once per run() call, its time and
+            # bytes spread over the call's steps
+            form, shape = PCS[c]
+            st = [k for k in ks if k.startswith('pc_step_halo') and ks[k].get('trace')]
+            if not st:
+                continue
+            st = max(st, key=lambda n: ks[n]['trace']['calls'])
+            fi = [k for k in ks if k.startswith('pc_halo_finish') and ks[k].get('trace')]
+            hb = ks[st].get('hbm_bytes_per_dispatch')
+            rec = {'shape': shape, 'kernels': [st] + fi[:1],
+                   'kernel_us_rocprof': {'step': ks[st]['trace'].get('median_us', ks[st]['trace']['avg_us'])},
+                   'hbm_bytes_per_step': hb, 'source': f'{tag}_pmc_summary.json'}
+            if fi and hb:
+                f = ks[fi[0]]
+                per = f['trace']['calls'] / ks[st]['trace']['calls']
+                rec['kernel_us_rocprof']['finish_per_step'] = per * f['trace'].get('median_us', f['trace']['avg_us'])
+                if f.get('hbm_bytes_per_dispatch'):
+                    rec['hbm_bytes_per_step'] = hb + per * f['hbm_bytes_per_dispatch']
+            traffic['pose_cell'][form] = rec
         elif c in PCS:
             form, shape = PCS[c]
             ex = [k for k in ks if k.startswith('pc_excite') and ks[k].get('trace')]
@@ -184,7 +204,7 @@ def main():
     if f:
         shutil.copy(f, os.path.join(raw, 'bench_kernel_stats.csv'))
     for c, rec in list(traffic['scans'].items()) + list(traffic['pose_cell'].items()):
-        cfg = c if c in SCANS else {'rows': 'pc64', 'cols': 'pc128'}[c]
+        cfg = c if c in SCANS else {'rows': 'pc64', 'halo': 'pc64', 'cols': 'pc128'}[c]
         rec['kernel_us_source'] = (f'profiles/{a.tag}/{cfg}_kernel_trace.csv (median over the dispatches; '
                                    f'the --stats average is kernel_us_rocprof_avg, {cfg}_kernel_stats.csv)')
         rec['counter_source'] = f'profiles/{a.tag}/{cfg}_counters.csv'
