@@ -2025,9 +2025,6 @@ constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;
 constexpr int HF_YJ = HF_W * HF_Q + 10;       // y-pass outputs per layer (pitch: the x pass reads conflict-free)
 constexpr int HF_QJ = HF_Q * HF_Q + 4;        // Q window per layer
 constexpr int HF_EXP_MAX = 64;                // steps whose keys pc_halo_finish exports itself
-#ifndef HF_YX_DPP
-#define HF_YX_DPP 0  // 1: y and x passes fused by DPP row shifts (measured slower: 1.56 + 1.20 vs 0.92 + 1.04 us)
-#endif
 
 // One step's control, a kernel argument (formed on the host by make_ctl_halo).
 struct PcCtlHalo {
@@ -2039,11 +2036,6 @@ struct PcCtlHalo {
     int wrap;                    // the union is a whole period in x or y (windows wrap inside it)
 };
 typedef float hf_f2 __attribute__((ext_vector_type(2)));  // (excitatory, inhibitory) pairs: packed FMAs
-// lane l + A's value within each 16-lane row (DPP row_shl:A; 0 past the row's end)
-template <int A>
-__device__ inline float hf_row_shl(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x100 + A, 0xF, 0xF, true));
-}
 
 // The normalisation total of a step from its per-block partials, formed by every wave
 // itself in one fixed order (so every block gets the same bits): 4 per lane, then DPP.
@@ -2343,67 +2335,6 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     co_lds_barrier();
     PC_STAMP(7, 2);
 
-#if HF_YX_DPP
-    // 3+4. y and x passes fused, one 16-lane DPP row per layer (4 layers per wave, 36
-    //    layers = 9 waves): lane rx of layer j's row forms its window row's y pass (10
-    //    outputs of each Gaussian) in registers; the x pass then takes rows rx .. rx+6
-    //    from the row's next lanes by DPP row_shl (which never leaves the 16-lane row),
-    //    so Q row qa = rx (lanes rx < 10) is formed with no LDS round trip or barrier
-    //    between the passes; the inhibition (:339-340) and the partial sum over the
-    //    layer's shifted own tile (Q rows / columns 3 .. 3+tw) follow.  Q goes to the
-    //    (dead) union image.
-    float* s_q = s_b;
-    double qs = 0.0;
-    {
-        static_assert(HF_NW * 4 == TH && HF_W == 16, "one DPP row of 16 lanes per layer");
-        const int j = wave * 4 + (lane >> 4), rx = lane & 15;
-        const co_f4* rw = reinterpret_cast<const co_f4*>(s_tw + j * HF_WJ + rx * HF_WP);
-        hf_f2 w[HF_W];   // (e, i) of the row's 16 cells
-#pragma unroll
-        for (int q = 0; q < HF_W / 2; ++q) {
-            const co_f4 a = rw[q];
-            w[2 * q] = hf_f2{a.x, a.y};
-            w[2 * q + 1] = hf_f2{a.z, a.w};
-        }
-        float ye[HF_Q], yi[HF_Q];
-#pragma unroll
-        for (int c = 0; c < HF_Q; ++c) {
-            hf_f2 eg = {0.f, 0.f};
-#pragma unroll
-            for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[c + t2];
-            ye[c] = eg.x;
-            yi[c] = eg.y;
-        }
-        const bool orow = (unsigned)(rx - HALF) < (unsigned)tw;
-#pragma unroll
-        for (int qc = 0; qc < HF_Q; ++qc) {
-            // rows rx .. rx + 6 of the same layer (lanes past the row's end read 0)
-            const float de[FL] = {ye[qc], hf_row_shl<1>(ye[qc]), hf_row_shl<2>(ye[qc]), hf_row_shl<3>(ye[qc]),
-                                  hf_row_shl<4>(ye[qc]), hf_row_shl<5>(ye[qc]), hf_row_shl<6>(ye[qc])};
-            const float di[FL] = {yi[qc], hf_row_shl<1>(yi[qc]), hf_row_shl<2>(yi[qc]), hf_row_shl<3>(yi[qc]),
-                                  hf_row_shl<4>(yi[qc]), hf_row_shl<5>(yi[qc]), hf_row_shl<6>(yi[qc])};
-            float e = 0.f, g = 0.f;
-#pragma unroll
-            for (int a = 0; a < FL; ++a) {
-                e += k.ge[a] * de[a];
-                g += k.gi[a] * di[a];
-            }
-            const float v = (e - g) * k.scale;
-            const float q = (v < k.inhib) ? 0.f : v - k.inhib;
-            if (rx < HF_Q) {
-                const bool own = orow && (unsigned)(qc - HALF) < (unsigned)tht;
-                if (own) qs += (double)q;
-                if constexpr (EXC) {
-                    if (own) Uo[((size_t)(x0 + rx - HALF) * Y + (y0 + qc - HALF)) * TH + j] = q;
-                } else {
-                    s_q[j * HF_QJ + rx * HF_Q + qc] = q;
-                }
-            }
-        }
-    }
-    PC_STAMP(7, 3);
-    float* s_po = s_t;   // the path outputs, into the (dead) theta-pass windows
-#else
     // 3. y pass: task (layer j, window row rx) -> 10 outputs of each Gaussian
     float* s_ye = s_b;
     float* s_yi = s_b + TH * HF_YJ;
@@ -2465,7 +2396,6 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     }
     float* s_po = s_b;
-#endif
     if constexpr (!EXC) {
         co_lds_barrier();
         PC_STAMP(7, 4);
