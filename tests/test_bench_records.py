@@ -37,3 +37,36 @@ def test_scan_roofline_fraction_is_physical():
     other = json.loads(json.dumps(tj))
     other['scans']['headline']['kernel'] = 'vt_scan_plane_kernel<32, false>'
     assert bench.scan_roofline(tv, other, 'headline')['frac'] is None
+
+
+def test_pose_cell_records_name_the_default_step_kernels():
+    """The 64x64x36 record is the halo form's one step kernel (the bench's default form
+    there), with PMC bytes per step of the order of the 24 B/cell the survey prices and a
+    kernel time that fits the measured wall per step; the 128x128x72 record is the column
+    form's excite + path pair."""
+    tj = _traffic()
+    halo = tj['pose_cell']['halo']
+    assert halo['shape'] == [64, 64, 36]
+    assert halo['kernels'][0].startswith('pc_step_halo<false>')
+    cells = 64 * 64 * 36
+    assert 0.25 * 24 * cells < halo['hbm_bytes_per_step'] < 4 * 24 * cells
+    assert 5.0 < halo['kernel_us_rocprof']['step'] < 20.0
+    cols = tj['pose_cell']['cols']
+    assert cols['shape'] == [128, 128, 72]
+    assert [k.split('<')[0] for k in cols['kernels']] == ['pc_excite_cols', 'pc_path_cols']
+
+
+def test_pmc_collect_halo_record():
+    """tools/pmc_collect.py turns a profiled halo run (step kernel per step, the finishing
+    kernel once per call) into per-step time and bytes."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location('pmc_collect', os.path.join(ROOT, 'tools', 'pmc_collect.py'))
+    pc = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pc)
+    ks = {'pc_step_halo<false>': {'trace': {'calls': 400, 'avg_us': 9.2, 'median_us': 9.0},
+                                  'hbm_bytes_per_dispatch': 2.0e6},
+          'pc_halo_finish': {'trace': {'calls': 4, 'avg_us': 4.0, 'median_us': 4.0},
+                             'hbm_bytes_per_dispatch': 1.0e6}}
+    rec = pc.traffic_of({'pc64': ks}, 'tag')['pose_cell']['halo']
+    assert rec['kernel_us_rocprof'] == {'step': 9.0, 'finish_per_step': 0.04}
+    assert abs(rec['hbm_bytes_per_step'] - (2.0e6 + 0.01 * 1.0e6)) < 1e-6
