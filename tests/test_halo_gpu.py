@@ -95,12 +95,14 @@ def test_network_death_vs_reference(halo):
     assert np.abs(b.posecells - dense_state(case, len(odom) - 1)).max() < F32_TOL
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (17, 30, 36), (16, 16, 36)])
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (17, 30, 36), (16, 16, 36), (128, 72, 36)])
 def test_random_and_fast_odometry_vs_oracle(halo, shape):
     """Bench odometry mixed with fast steps (vtrans up to 2 m: shifts up to 10 cells,
     unions beyond the LDS-DMA image, which take the direct-load path), ragged tiles
-    (17 x 30) and a grid of exactly one window (16 x 16); run() in batches of 7 so
-    every batch starts from a normalised state and ends in pc_halo_finish."""
+    (17 x 30), a grid of exactly one window (16 x 16) and one of 576 tiles (more than
+    one block per CU and per argmax slot, RS_PC_FORM=halo beyond the default's range);
+    run() in batches of 7 so every batch starts from a normalised state and ends in
+    pc_halo_finish."""
     r = np.random.default_rng(41)
     n = 28
     od = np.stack([np.where(r.random(n) < 0.6, r.uniform(0, 0.6, n), r.uniform(0.9, 2.0, n)),
