@@ -2004,11 +2004,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 //    and that Q needs P on the 16 x 16 window around it.  The excitation runs theta
 //    pass first: the union of the step's shifted 16 x 16 windows goes global -> LDS
 //    by LDS-DMA (each cell's theta column is contiguous, theta-fastest C order, so the
-//    pieces are whole 1 KiB runs per wave-instruction), a thread then takes one
-//    cell's column, scales it, forms all TH theta-pass outputs in registers and
-//    stores those of the windows that hold the cell; then per layer on its own
-//    window the y pass (16 x 10), the x pass (10 x 10) with the inhibition, the 7 x 7
-//    path filter and clamp, the theta filter and clamp, and the write-through store.
+//    pieces are whole 1 KiB runs per wave-instruction); the theta pass reads it in
+//    place, a lane per window cell through a run of layers (phase 2 below); then per
+//    layer on its own window the y pass (16 x 10), the x pass (10 x 10) with the
+//    inhibition, the 7 x 7 path filter and clamp, the theta filter and clamp, and the
+//    write-through store.
 //  * The partial sums cover, for layer j, the block's tile shifted by layer j's
 //    shift (the centre of its Q window): those shifted tiles partition each layer as
 //    the tiles do.
