@@ -2036,6 +2036,10 @@ struct PcCtlHalo {
     int wrap;                    // the union is a whole period in x or y (windows wrap inside it)
 };
 typedef float hf_f2 __attribute__((ext_vector_type(2)));  // (excitatory, inhibitory) pairs: packed FMAs
+// two 16-bit fields in one kernel argument (pc_step_halo's preloaded union origin / extent)
+inline int hf_pack(short lo, short hi) {
+    return (int)((unsigned)(unsigned short)lo | ((unsigned)(unsigned short)hi << 16));
+}
 
 // The normalisation total of a step from its per-block partials, formed by every wave
 // itself in one fixed order (so every block gets the same bits): 4 per lane, then DPP.
@@ -2053,12 +2057,18 @@ __device__ inline double pc_partials_total(const double* __restrict__ part, int 
 
 // EXC: excitation only (rs_pc_excite, the step the reference runs before a LUT
 // KeyError): zero shifts, Q of the own cells stored into Uo (theta-fastest), partials.
+// The first HF_PRELOAD arguments are everything the union image's LDS-DMA addresses
+// need (the state, the grid, the block count, the union's origin and extent packed
+// as 16-bit pairs): posecell.hip is built with -amdgpu-kernarg-preload-count, so they
+// arrive in scalar registers with the wave and the image's loads issue without a
+// kernel-argument round trip (two dependent ones before: the block count, then the
+// union, 0.84 us from the block's start to the DMA issue at 64 x 64 x 36).
 template <bool EXC>
 __global__ __launch_bounds__(HF_NT) void pc_step_halo(
-    const float* __restrict__ U, float* __restrict__ Uo, const double* __restrict__ part_in,
-    int npart_in, double* __restrict__ part_out, unsigned long long* __restrict__ slot_prev,
-    unsigned long long* __restrict__ slot_zero, const float* __restrict__ filt, int nf, PcCtlHalo ctl,
-    int X, int Y, int gx, SepKernel<float> k) {
+    const float* __restrict__ U, int X, int Y, int gx, int nblk, int ulo, int uext, float* __restrict__ Uo,
+    const double* __restrict__ part_in, int npart_in, double* __restrict__ part_out,
+    unsigned long long* __restrict__ slot_prev, unsigned long long* __restrict__ slot_zero,
+    const float* __restrict__ filt, int nf, PcCtlHalo ctl, SepKernel<float> k) {
     constexpr int TH = HF_TH, NV = TH / 4;   // 16-byte pieces per theta column
     static_assert(TH % 4 == 0, "theta columns of whole 16-byte pieces");
     constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
@@ -2076,11 +2086,12 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     __shared__ unsigned long long s_bk[HF_NW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int tile = st_tile(blockIdx.x, gridDim.x);
+    const int tile = st_tile(blockIdx.x, nblk);
     const int x0 = (tile % gx) * HF_T, y0 = (tile / gx) * HF_T;
     const int tw = min(HF_T, X - x0), tht = min(HF_T, Y - y0);
-    const int UW = ctl.uw, UH = ctl.uh, nu = UW * UH;
-    const int ux0 = co_wrap(x0 - 2 * HALF + ctl.ux, X), uy0 = co_wrap(y0 - 2 * HALF + ctl.uy, Y);
+    const int cux = (short)(ulo & 0xFFFF), cuy = ulo >> 16;   // the union's origin (centred shifts)
+    const int UW = uext & 0xFFFF, UH = uext >> 16, nu = UW * UH;
+    const int ux0 = co_wrap(x0 - 2 * HALF + cux, X), uy0 = co_wrap(y0 - 2 * HALF + cuy, Y);
     const bool dma = nu <= HF_UMAX;
     PC_STAMP(7, 0);
     // 1. the union image, issued first: piece p = tid + HF_NT * r is 16-byte piece p % NV
@@ -2115,6 +2126,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
         }
     }
+    PC_STAMP(3, 0);
     // the normalisation of the state entering the step, the filter table, the control
     // (lane L of every wave holds layer L's window start, read by readlane in phase 2)
     const int lsx = ctl.sx[lane < TH ? lane : 0], lsy = ctl.sy[lane < TH ? lane : 0];
@@ -2126,6 +2138,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     if (slot_zero != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += HF_NT) st_wt(&slot_zero[i], 0ull);  // the next launch max-reduces into them
     if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces have landed
+    PC_STAMP(3, 1);
     co_lds_barrier();
     PC_STAMP(7, 1);
 
@@ -2238,7 +2251,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             // wave 8: the argmax of the state entering the step over the own tile (lane:
             // cell lane & 15, quads lane >> 4 + 4 m)
             const int i = (lane & 15) >> 2, jc = lane & 3;
-            int cu = co_wrap(2 * HALF - ctl.ux, X) + i, cv = co_wrap(2 * HALF - ctl.uy, Y) + jc;
+            int cu = co_wrap(2 * HALF - cux, X) + i, cv = co_wrap(2 * HALF - cuy, Y) + jc;
             cu -= cu >= X ? X : 0;
             cv -= cv >= Y ? Y : 0;
             if (i < tw && jc < tht && cu < UW && cv < UH) {
@@ -2318,7 +2331,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     if (want_key && tid < tw * tht) {
         // an own cell outside the union (a large uniform shift): its key from memory
         const int i = tid / tht, j = tid - i * tht;
-        int cu = co_wrap(2 * HALF - ctl.ux, X) + i, cv = co_wrap(2 * HALF - ctl.uy, Y) + j;
+        int cu = co_wrap(2 * HALF - cux, X) + i, cv = co_wrap(2 * HALF - cuy, Y) + j;
         cu -= cu >= X ? X : 0;
         cv -= cv >= Y ? Y : 0;
         if (cu >= UW || cv >= UH) {
@@ -2988,12 +3001,12 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         PcCtlHalo c;
         make_ctl_halo(h, s, ox, oy, fidx, zf, &c);
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
-        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[s & 1], buf[(s + 1) & 1],
+        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[s & 1], h->X, h->Y,
+                           h->cgx, (int)grid.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), buf[(s + 1) & 1],
                            h->dPart + (size_t)((s + 1) & 1) * h->nPart, s == 0 ? 0 : h->nPart,
                            h->dPart + (size_t)(s & 1) * h->nPart,
                            s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
-                           h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->X,
-                           h->Y, h->cgx, h->kf);
+                           h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->kf);
         RS_HIP(hipGetLastError());
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
     }
@@ -3719,9 +3732,9 @@ int rs_pc_excite(rs_pc* h) {
         c.uw = (short)HF_W;
         c.uh = (short)HF_W;
         hipLaunchKernelGGL((pc_step_halo<true>), dim3(h->cgx * h->cgy), dim3(HF_NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), static_cast<float*>(h->dQ), h->dPart, 0, h->dPart,
-                           nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->X, h->Y, h->cgx,
-                           h->kf);
+                           static_cast<const float*>(h->dP), h->X, h->Y, h->cgx, h->cgx * h->cgy,
+                           hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), static_cast<float*>(h->dQ), h->dPart, 0,
+                           h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf);
         RS_HIP(hipGetLastError());
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);

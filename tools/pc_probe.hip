@@ -3,7 +3,7 @@
 // stamps (100 MHz) at their phase boundaries, then reports per-phase times
 // over the blocks of one step, and back-to-back launch costs of each kernel
 // alone and of an empty kernel with the same grid.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ipyratslam_amd/csrc \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-kernarg-preload-count=7 -Iinclude -Ipyratslam_amd/csrc \
 //         tools/pc_probe.hip pyratslam_amd/csrc/rs_common.cpp -o /tmp/pc_probe
 #include <hip/hip_runtime.h>
 
@@ -162,6 +162,17 @@ int main(int argc, char** argv) {
         }
         printf("   halo phase 2: barrier end -> task loop %.2f us, task loop %.2f us (wave 0, median)\n",
                median(a) * 1e-3, median(b) * 1e-3);
+        {
+            std::vector<double> i1, w1;
+            for (int bb = 0; bb < h->nPart; ++bb) {
+                const unsigned long long* r3 = &st[((size_t)3 * 4096 + bb) * 8];
+                const unsigned long long* r7 = &st[((size_t)7 * 4096 + bb) * 8];
+                i1.push_back((double)(r3[0] - r7[0]) * 10.0);
+                w1.push_back((double)(r3[1] - r7[0]) * 10.0);
+            }
+            printf("   halo phase 1 (wave 0): LDS-DMA issued after %.2f us, landed after %.2f us (median)\n",
+                   median(i1) * 1e-3, median(w1) * 1e-3);
+        }
         printf("   halo phase 2 per wave, task loop end after phase 1 (median us):");
         for (int w = 0; w < 9; ++w) {
             std::vector<double> c;
@@ -200,9 +211,10 @@ int main(int argc, char** argv) {
         make_ctl_halo(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, (float*)h->dQ,
+            hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, X, Y, h->cgx,
+                               (int)g.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), (float*)h->dQ,
                                h->dPart, h->nPart, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
-                               (const float*)h->dFilt, h->nf, c, X, Y, h->cgx, h->kf);
+                               (const float*)h->dFilt, h->nf, c, h->kf);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
