@@ -1337,10 +1337,10 @@ __device__ inline CoLayers<CHUNK> co_layers(int ch, int KC, int TH) {
 // if the rows were contiguous, so the theta pass's 16-byte reads of consecutive groups
 // of consecutive cells are conflict-free)
 template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, int FIX_TH = 0>
-__global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ P, T* __restrict__ Q,
+__global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ P, int X, int Y, int TH,
+                                                          int gx, int gy, int nblk, T* __restrict__ Q,
                                                           double* __restrict__ part,
-                                                          unsigned long long* __restrict__ res_slot,
-                                                          int X, int Y, int TH, int gx, int gy, int KC,
+                                                          unsigned long long* __restrict__ res_slot, int KC,
                                                           SepKernel<T> k) {
     constexpr int NT = 64 * NW, HX = TX + 2 * HALF, HY = TY + 2 * HALF;
     constexpr int VEC = co_vec<T>();
@@ -1353,7 +1353,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     __shared__ double s_red[NW];
     using V = typename CoVec<T>::type;
     const int tid = threadIdx.x;
-    const int tile = st_tile(blockIdx.x, gridDim.x), xy = tile % (gx * gy);
+    const int tile = st_tile(blockIdx.x, nblk), xy = tile % (gx * gy);
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     if (res_slot != nullptr && blockIdx.x == 0)
@@ -1575,9 +1575,9 @@ __device__ inline int co_wave_ext_i(int v) {
 // control's, the partials' and the filter table's loads: one round trip.
 template <typename T, int TX, int TY, int NW, int THM, bool CHUNK, typename CTL, int DMA_TH = 0>
 __global__ __launch_bounds__(64 * NW) void pc_path_cols(
-    const T* __restrict__ Q, T* __restrict__ P, const double* __restrict__ part, int npart,
-    const T* __restrict__ filt, int nf, CTL ctl, unsigned long long* __restrict__ res_slot,
-    T* __restrict__ bmax, unsigned* __restrict__ bidx, int X, int Y, int TH, int gx, int gy, int KC) {
+    const T* __restrict__ Q, int X, int Y, int TH, int gx, int gy, int nblk, T* __restrict__ P,
+    const double* __restrict__ part, int npart, const T* __restrict__ filt, int nf, CTL ctl,
+    unsigned long long* __restrict__ res_slot, T* __restrict__ bmax, unsigned* __restrict__ bidx, int KC) {
     constexpr int NT = 64 * NW, VEC = co_vec<T>();
     constexpr bool DMA = DMA_TH > 0;
     // Q is theta-fastest, like P: the block loads the union of its layers' shifted
@@ -1606,7 +1606,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     __shared__ T s_bv[NW];
     __shared__ unsigned s_bl[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tile = st_tile(blockIdx.x, gridDim.x), xy = tile % (gx * gy);
+    const int tile = st_tile(blockIdx.x, nblk), xy = tile % (gx * gy);
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
     PC_STAMP(6, 0);
@@ -3123,20 +3123,20 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
         if constexpr (std::is_same<T, float>::value) {
             if (whole && h->TH == CO_DMA_TH) {  // configs[3]'s theta extent
                 hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, CO_DMA_TH>), g,
-                                   dim3(64 * CO_NW), 0, h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH,
-                                   h->cgx, h->cgy, h->coKC, k);
+                                   dim3(64 * CO_NW), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                                   (int)g.x, Q, h->dPart, slot, h->coKC, k);
                 fixed = true;
             }
         }
         if (fixed) {
         } else if (whole)
             hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false>), g, dim3(64 * co_nw<T>()), 0,
-                               h->stream, P, Q, h->dPart, slot, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                               h->stream, P, h->X, h->Y, h->TH, h->cgx, h->cgy, (int)g.x, Q, h->dPart, slot,
                                h->coKC, k);
         else
             hipLaunchKernelGGL((pc_excite_cols<T, CO_TX, CO_TY, CO_NW_CHUNK, THC, true>), g,
-                               dim3(64 * CO_NW_CHUNK), 0, h->stream, P, Q, h->dPart, slot, h->X, h->Y,
-                               h->TH, h->cgx, h->cgy, h->coKC, k);
+                               dim3(64 * CO_NW_CHUNK), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                               (int)g.x, Q, h->dPart, slot, h->coKC, k);
         RS_HIP(hipGetLastError());
         if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
         if (!ctl) return RS_OK;
@@ -3146,22 +3146,22 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
             // TH == 72 (configs[3]): the LDS-DMA window instance
             if (whole && h->TH == CO_DMA_TH) {
                 hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, PcCtlInline, CO_DMA_TH>),
-                                   g, dim3(64 * CO_NW), 0, h->stream, Q, static_cast<T*>(h->dP), h->dPart,
-                                   h->nPart, filt, h->nf, *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx,
-                                   h->cgy, h->coKC);
+                                   g, dim3(64 * CO_NW), 0, h->stream, Q, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                                   (int)g.x, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
+                                   bmax, bidx, h->coKC);
                 launched = true;
             }
         }
         if (launched) {
         } else if (whole)
             hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, co_nw<T>(), THF, false, CTL>), g, dim3(64 * co_nw<T>()), 0,
-                               h->stream, Q, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf,
-                               *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx, h->cgy, h->coKC);
+                               h->stream, Q, h->X, h->Y, h->TH, h->cgx, h->cgy, (int)g.x, static_cast<T*>(h->dP),
+                               h->dPart, h->nPart, filt, h->nf, *ctl, slot, bmax, bidx, h->coKC);
         else
             hipLaunchKernelGGL((pc_path_cols<T, CO_TX, CO_TY, CO_NW_CHUNK, THC, true, CTL>), g,
-                               dim3(64 * CO_NW_CHUNK), 0, h->stream, Q, static_cast<T*>(h->dP), h->dPart,
-                               h->nPart, filt, h->nf, *ctl, slot, bmax, bidx, h->X, h->Y, h->TH, h->cgx,
-                               h->cgy, h->coKC);
+                               dim3(64 * CO_NW_CHUNK), 0, h->stream, Q, h->X, h->Y, h->TH, h->cgx, h->cgy,
+                               (int)g.x, static_cast<T*>(h->dP), h->dPart, h->nPart, filt, h->nf, *ctl, slot,
+                               bmax, bidx, h->coKC);
     } else if (h->streamed) {
         RS_TRY((pc_launch_stream<T, CTL>(h, P, Q, slot, bmax, bidx, ctl, prof_base)));
     } else if (h->tiling == 64 || h->tiling == 128) {

@@ -246,8 +246,8 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
             hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, THF, false>), g, b, 0, h->stream,
-                               (const float*)h->dP, (float*)h->dQ, h->dPart, h->dRes, X, Y, TH, h->cgx,
-                               h->cgy, h->coKC, h->kf);
+                               (const float*)h->dP, X, Y, TH, h->cgx, h->cgy, (int)g.x, (float*)h->dQ,
+                               h->dPart, h->dRes, h->coKC, h->kf);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
@@ -255,9 +255,9 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
             hipLaunchKernelGGL((pc_path_cols<float, CO_TX, CO_TY, CO_NW, THF, false, PcCtlRing>), g, bp, 0, h->stream,
-                               (const float*)h->dQ, (float*)h->dP, h->dPart, h->nPart,
-                               (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
-                               (unsigned*)nullptr, X, Y, TH, h->cgx, h->cgy, h->coKC);
+                               (const float*)h->dQ, X, Y, TH, h->cgx, h->cgy, (int)g.x, (float*)h->dP, h->dPart,
+                               h->nPart, (const float*)h->dFilt, h->nf, ctl, h->dRes, (float*)nullptr,
+                               (unsigned*)nullptr, h->coKC);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
