@@ -2098,32 +2098,42 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     //    of union cell p / NV (cells row-major, UH per row), landing at s_b + 4p
     if (dma) {
         constexpr int DC = HF_NT / NV, DL = HF_NT % NV, NR = (HF_UMAX * NV + HF_NT - 1) / HF_NT;
-        const int npc = nu * NV, dU = DC / UH, dV = DC - dU * UH;
+        // A lane walks its pieces with full-rate 32-bit arithmetic only (no 64-bit,
+        // quarter-rate address math; measured neutral: the issue, about 0.95 us from the
+        // block's start at 64 x 64 x 36, is bound by the CU's 64 B/clk path for the
+        // block's ~70 KB image, not by the VALU, r4 probe): the row's first cell rb =
+        // gr * Y carried incrementally (the union row advances by dU or dU + 1 < X per
+        // round and UW <= X, so one wrap suffices), a 32-bit byte offset from the state's
+        // base (n * 4 <= INT_MAX, pc_halo_fit) by a 24-bit multiply (cells < 2^24)
+        const int npc = nu * NV, dU = DC / UH, dV = DC - dU * UH, XY = X * Y;
         int c = tid / NV, l4 = tid - c * NV, ui = c / UH, vi = c - ui * UH;
+        int rb = ux0 + ui;
+        rb = (rb >= X ? rb - X : rb) * Y;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
             const int i0 = r * HF_NT + wave * 64;  // wave-uniform
             if (i0 < npc) {
                 if (i0 + lane < npc) {
-                    int gr = ux0 + ui, gc = uy0 + vi;
-                    gr -= gr >= X ? X : 0;
+                    int gc = uy0 + vi;
                     gc -= gc >= Y ? Y : 0;
+                    const unsigned boff = __umul24((unsigned)(rb + gc), (unsigned)(4 * TH)) + 16u * (unsigned)l4;
                     __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) const void*)(U + ((unsigned)gr * Y + gc) * TH + 4 * l4),
+                        (__attribute__((address_space(1))) const void*)(reinterpret_cast<const char*>(U) + boff),
                         (__attribute__((address_space(3))) void*)(s_b + 4 * i0), 16, 0, 0);
                 }
             }
             l4 += DL;
             vi += dV;
-            ui += dU;
+            rb += dU * Y;
             if (l4 >= NV) {
                 l4 -= NV;
                 ++vi;
             }
             if (vi >= UH) {
                 vi -= UH;
-                ++ui;
+                rb += Y;
             }
+            rb -= rb >= XY ? XY : 0;
         }
     }
     PC_STAMP(3, 0);
