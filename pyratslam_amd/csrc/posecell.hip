@@ -2100,8 +2100,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         constexpr int DC = HF_NT / NV, DL = HF_NT % NV, NR = (HF_UMAX * NV + HF_NT - 1) / HF_NT;
         // A lane walks its pieces with full-rate 32-bit arithmetic only (no 64-bit,
         // quarter-rate address math; measured neutral: the issue, about 0.95 us from the
-        // block's start at 64 x 64 x 36, is bound by the CU's 64 B/clk path for the
-        // block's ~70 KB image, not by the VALU, r4 probe): the row's first cell rb =
+        // block's start at 64 x 64 x 36, is not VALU-bound, r4 probe): the row's first cell rb =
         // gr * Y carried incrementally (the union row advances by dU or dU + 1 < X per
         // round and UW <= X, so one wrap suffices), a 32-bit byte offset from the state's
         // base (n * 4 <= INT_MAX, pc_halo_fit) by a 24-bit multiply (cells < 2^24)
