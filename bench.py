@@ -322,6 +322,27 @@ def pc_roofline(ncell, us_per_step, traffic=None):
             'note': '24 B/cell/step algorithmic (SURVEY 8(d)) / wall time per batched step'}
 
 
+def pc_kernel_rooflines(shape, kus, rec):
+    """Per-kernel HBM rates from a profile record: each step kernel reads one float32
+    volume and writes one (8 algorithmic B per cell) in its rocprof trace median; with
+    the PMC bytes of that kernel (FETCH doubled per MI355X_MICROARCH.md + WRITE) where
+    the record holds them."""
+    ncell = shape[0] * shape[1] * shape[2]
+    pmc = rec.get('hbm_bytes_per_kernel') or {}
+    out = {}
+    for name, us in kus.items():
+        if us < 0.1:   # a once-per-call kernel amortised over the batch
+            continue
+        k = {'us_rocprof_median': us, 'algorithmic_bytes': 8.0 * ncell,
+             'algorithmic_GBs': 8.0 * ncell / (us * 1e-6) / 1e9}
+        k['algorithmic_frac'] = k['algorithmic_GBs'] / HBM_PEAK_GBS
+        if name in pmc:
+            k['pmc_bytes'] = pmc[name]
+            k['pmc_GBs'] = pmc[name] / (us * 1e-6) / 1e9
+        out[name] = k
+    return out
+
+
 def bench_posecell_stress(args, d):
     """configs[3]: the 128x128x72 grid, batched run() steps/s and kernel roofline."""
     from pyratslam_amd import PoseCellNetwork, synthetic
@@ -337,7 +358,7 @@ def bench_posecell_stress(args, d):
     t1 = time.perf_counter()
     d.barrier()
     dt = d.max(t1 - t0)
-    dev_us = _device_us_per_step(net, od, n)
+    dev_us = _device_us_per_step(net, od, 50, n)
     finite = bool(np.isfinite(net.posecells).all())
     form = net.step_form()
     net.close()
@@ -348,15 +369,18 @@ def bench_posecell_stress(args, d):
             'roofline': pc_roofline(ncell, 1e6 * dt / n)}
 
 
-def _device_us_per_step(net, od, n):
-    """Device time per batched step: two HIP events around one whole run() of n steps
-    (no event between the launches, so nothing is added between the kernels), after
-    the same warm run: at most the wall time per step beside it."""
+def _device_us_per_step(net, od, start, n):
+    """Device time per batched step: two HIP events around one whole run() of the n
+    steps od[start:start + n] (no event between the launches, so nothing is added
+    between the kernels), after the same warm run: at most the wall time per step
+    beside it."""
+    steps = od[start:start + n]
+    assert start >= 0 and len(steps) == n, (start, n, len(od))
     net.set_profiling(True, per_kernel=False)
-    net.run(od[50:50 + n])
+    net.run(steps)
     ms = net.device_ms()
     net.set_profiling(False)
-    return 1e3 * ms / n
+    return 1e3 * ms / len(steps)
 
 
 def bench_posecells(args, d):
@@ -380,7 +404,7 @@ def bench_posecells(args, d):
     for v in od[base + 16:base + 16 + args.pc_calls]:
         net.update(v)
     c1 = time.perf_counter()
-    dev_us = _device_us_per_step(net, od[args.pc_warmup - 50:], args.pc_steps)
+    dev_us = _device_us_per_step(net, od, args.pc_warmup, args.pc_steps)
     ncell = shape[0] * shape[1] * shape[2]
     finite = bool(np.isfinite(net.posecells).all())
     form = net.step_form()
@@ -638,12 +662,15 @@ def main():
             if rec.get('shape') in (None, leg['shape']):
                 leg['roofline']['traffic'] = rec.get('hbm_bytes_per_step')
                 leg['roofline']['traffic_kernels'] = rec.get('kernels')
-                # the profiles' per-kernel trace medians, only where they fit inside the
-                # wall time per step they sit beside (a profiled run's kernels need not
-                # be the timed steps' kernels)
+                # the profiles' per-kernel trace medians, with the record they come from
+                # and whether their sum exceeds the wall time per step beside them (a
+                # profiled run's kernels need not be the timed steps' kernels)
                 kus = rec.get('kernel_us_rocprof')
-                if kus and sum(kus.values()) <= leg['us_per_step']:
+                if kus:
                     leg['kernel_us_per_step_rocprof'] = kus
+                    leg['kernel_us_rocprof_source'] = rec.get('kernel_us_source')
+                    leg['kernel_us_rocprof_exceeds_wall'] = sum(kus.values()) > leg['us_per_step']
+                    leg['roofline']['kernels'] = pc_kernel_rooflines(leg['shape'], kus, rec)
     out = {
         'metric': METRIC,
         'value': tv['value'],

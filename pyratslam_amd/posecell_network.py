@@ -375,7 +375,10 @@ class PoseCellNetwork:
         _lib.check(self._lib.rs_pc_set_profiling(self._h, 0 if not enable else (1 if per_kernel else 2)))
 
     def kernel_ms(self):
-        """(excite_ms, path_ms) summed over the steps of the last run (profiling on)."""
+        """Kernel times of the last run (profiling on, per_kernel=True), as
+        rs_pc_kernel_ms returns them: (excite_ms, path_ms) summed over the steps for
+        the two-launch forms (rows, tiles, cols, tc, stream); for the halo form
+        (step_ms, finish_ms): the step kernels summed, then the one pc_halo_finish."""
         ms = np.zeros(2)
         _lib.check(self._lib.rs_pc_kernel_ms(self._h, _lib.ptr(ms, ctypes.c_double)))
         return float(ms[0]), float(ms[1])

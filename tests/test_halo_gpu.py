@@ -304,3 +304,16 @@ def test_argmax_exact_ties(halo, case):
         own, p = own_argmax(net)
         assert own == want[-1]
         assert np.abs(p - ref.posecells).max() < F32_TOL
+
+
+def test_halo_refused_beyond_16bit_union_fields(pcn, monkeypatch):
+    """The union's origin and extent travel to the kernel as 16-bit fields
+    (make_ctl_halo / hf_pack): a grid with X or Y beyond 32767 is refused by the halo
+    form (a silent truncation would load the wrong cells), and the default form for
+    such a grid is another one."""
+    monkeypatch.setenv('RS_PC_FORM', 'halo')
+    for shape in ((32768, 16, 36), (16, 32768, 36)):
+        with pytest.raises(ValueError, match='32767'):
+            pcn(shape)
+    monkeypatch.delenv('RS_PC_FORM')
+    assert pcn((16, 32768, 36)).step_form() != 'halo'
