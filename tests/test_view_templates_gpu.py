@@ -420,7 +420,7 @@ def test_untimed_scans(vtmod):
     assert lib.device_ms() > 0.0
 
 
-@pytest.mark.parametrize('t,nb,q', [(1000, 4, 256), (70, 3, 33), (0, 2, 5)])
+@pytest.mark.parametrize('t,nb,q', [(1000, 4, 256), (70, 3, 33), (0, 2, 5), (200, 37, 20)])
 def test_match_stream_equals_frozen_batches(vtmod, t, nb, q):
     """rs_vt_match_stream (nb batches, one host sync) == nb rs_vt_match_batch(FROZEN)
     calls, from host memory and from batches resident in HBM; the oracle pins scores."""
@@ -450,6 +450,26 @@ def test_match_stream_equals_frozen_batches(vtmod, t, nb, q):
             ref = V.vt_scores_library(lib_np, batches[b, i])
             assert score_h[b, i] == ref.min() and idx_h[b, i] == int(np.argmin(ref))
     assert lib.count() == t
+
+
+def test_match_stream_host_groups_reuse_and_grow(vtmod):
+    """Host batches go up in groups of 16 through two device buffers (the group
+    before last's buffer is reused only after its planes were built): calls of 1, 16,
+    17, 40 and again 3 batches of growing and shrinking size on one handle, each equal
+    to the same batches from HBM."""
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(300, 64, 32, seed=9)
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    lib.add(lib_np)
+    for nb, q in ((1, 64), (16, 8), (17, 64), (40, 30), (3, 100)):
+        batches = np.stack([V.synthetic_queries(lib_np, q, seed=1000 * nb + b)[0] for b in range(nb)])
+        idx_h, score_h = lib.match_stream(batches)
+        buf = _lib.DeviceBuffer(batches.nbytes).upload(batches)
+        idx_d, score_d = lib.match_stream((nb, q, buf))
+        buf.close()
+        assert np.array_equal(idx_h, idx_d) and np.array_equal(score_h, score_d), (nb, q)
+        ref = V.vt_scores_library(lib_np, batches[-1, -1])
+        assert score_h[-1, -1] == ref.min() and idx_h[-1, -1] == int(np.argmin(ref))
 
 
 def test_match_stream_refuses_host_reduced_shards(vtmod):
