@@ -2135,7 +2135,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             rb -= rb >= XY ? XY : 0;
         }
     }
-    PC_STAMP(3, 0);
+    PC_STAMP(10, 0);
     // the normalisation of the state entering the step, the filter table, the control
     // (lane L of every wave holds layer L's window start, read by readlane in phase 2)
     const int lsx = ctl.sx[lane < TH ? lane : 0], lsy = ctl.sy[lane < TH ? lane : 0];
@@ -2147,7 +2147,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     if (slot_zero != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += HF_NT) st_wt(&slot_zero[i], 0ull);  // the next launch max-reduces into them
     if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces have landed
-    PC_STAMP(3, 1);
+    PC_STAMP(10, 1);
     co_lds_barrier();
     PC_STAMP(7, 1);
 
@@ -2159,7 +2159,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     hf_f2 gei[FL];
 #pragma unroll
     for (int t = 0; t < FL; ++t) gei[t] = hf_f2{k.ge[t], k.gi[t]};
-    PC_STAMP(4, 0);
+    PC_STAMP(11, 0);
     if (dma && !ctl.wrap) {
         // the common case, read straight from the union image [cell][layer]: wave w < 8
         // takes window rows 4(w&3) .. +3 (a lane per window cell) through the layers
@@ -2335,8 +2335,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{});
         }
     }
-    PC_STAMP(4, 1);
-    PC_STAMPW(5);
+    PC_STAMP(11, 1);
+    PC_STAMPW(12);
     if (want_key && tid < tw * tht) {
         // an own cell outside the union (a large uniform shift): its key from memory
         const int i = tid / tht, j = tid - i * tht;
@@ -2612,7 +2612,15 @@ struct PcCtlTc {
     // chunk c's union of its G + 6 layers' shifted windows: origin (smallest centred
     // shift) and extent, packed as 16-bit pairs (lo: x, hi: y)
     int uorg[TC_NCH_MAX], uext[TC_NCH_MAX];
+    int urows;   // union rows held in LDS by this launch (the widest fitting chunk's UW)
 };
+
+// Dynamic LDS of the chunked path kernel for a union of `rows` rows: whole rows of
+// TC_UW cells of 4 (G/4 + 2) floats, plus one wave-instruction of slack for the last
+// LDS-DMA pieces.
+inline size_t tc_union_lds_bytes(int G, int rows) {
+    return ((size_t)rows * TC_UW * 4 * (G / 4 + 2) + 64 * 4) * sizeof(float);
+}
 
 template <int G>
 struct TcGeom {
@@ -2818,9 +2826,11 @@ __global__ __launch_bounds__(64 * NW) void pc_path_tc(const float* __restrict__ 
                                                       unsigned long long* __restrict__ res_slot) {
     using Gm = TcGeom<G>;
     constexpr int NT = 64 * NW, NU = Gm::NU, LU = Gm::LU, NL = Gm::NL;
-    constexpr int WIN = TC_UW * TC_UW * LU;   // union image [u][v][local layer], row pitch TC_UW cells
     constexpr int PP = LU;                    // filter outputs [cell][L], 16-byte aligned rows
-    __shared__ __attribute__((aligned(16))) float s_w[WIN + 64 * 4];
+    // the union image [u][v][local layer] (row pitch TC_UW cells), in dynamic LDS sized
+    // by the host for the step's widest chunk union (tc_union_lds_bytes): at small
+    // shifts more blocks share a CU
+    extern __shared__ __attribute__((aligned(16))) float s_w[];
     __shared__ __attribute__((aligned(16))) float s_p[TC_T * TC_T * PP];
     __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_dxy[NL], s_fo[NL];
@@ -2833,7 +2843,8 @@ __global__ __launch_bounds__(64 * NW) void pc_path_tc(const float* __restrict__ 
     // 1. the union of the chunk's layers' shifted 14 x 14 windows (host-formed)
     const int uorg = ctl.uorg[tl.ch], uext = ctl.uext[tl.ch];
     const int umx = (short)(uorg & 0xFFFF), umy = uorg >> 16, UW = uext & 0xFFFF, UH = uext >> 16;
-    const bool uni = UW <= TC_UW && UH <= TC_UW && UW <= X && UH <= Y;
+    // (ctl.urows: the union rows the launch's dynamic LDS holds, >= every fitting chunk's UW)
+    const bool uni = UW <= ctl.urows && UH <= TC_UW && UW <= X && UH <= Y;
     if (uni) {
         int gx0 = tl.x0 - HALF + umx, gy0 = tl.y0 - HALF + umy, u0 = (k0 >> 2) - 1;
         gx0 = co_wrap(gx0, X);
@@ -3418,6 +3429,14 @@ void make_ctl_tc(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, co
         c->uorg[ch] = hf_pack((short)mnx, (short)mny);
         c->uext[ch] = hf_pack((short)std::min(TC_W + mxx - mnx, 0x7FFF), (short)std::min(TC_W + mxy - mny, 0x7FFF));
     }
+    // the LDS rows this step's launch needs: the widest chunk union that fits the image
+    // (a wider chunk reads its windows from memory); at least one row
+    int rows = 1;
+    for (int ch = 0; ch < h->coNch; ++ch) {
+        const int uw = c->uext[ch] & 0xFFFF, uh = c->uext[ch] >> 16;
+        if (uw <= TC_UW && uh <= TC_UW && uw <= h->X && uh <= h->Y) rows = std::max(rows, uw);
+    }
+    c->urows = rows;
 }
 
 // The instantiated (G, NW) pairs of the theta-chunked kernels.
@@ -3446,7 +3465,8 @@ int pc_launch_tc(rs_pc* h, const StepOut& so, const PcCtlTc* ctl, int prof_base)
     done = false;
 #define PC_TC_PATH(g_, nw_)                                                                                   \
     if (!done && h->tcG == g_ && h->tcNW == nw_) {                                                          \
-        hipLaunchKernelGGL((pc_path_tc<g_, nw_>), g, dim3(64 * nw_), 0, h->stream, Q, h->X, h->Y, h->TH, h->cgx, \
+        hipLaunchKernelGGL((pc_path_tc<g_, nw_>), g, dim3(64 * nw_), tc_union_lds_bytes(g_, ctl->urows), h->stream, \
+                           Q, h->X, h->Y, h->TH, h->cgx,                                                    \
                            h->coNch, (int)g.x, static_cast<float*>(h->dP), h->dPart, h->nPart,              \
                            static_cast<const float*>(h->dFilt), h->nf, *ctl, so.slot);                      \
         done = true;                                                                                        \
@@ -3949,6 +3969,13 @@ int pc_tc_set(rs_pc* h, int G, int nw) {
     RS_CHECK(pc_tc_fit(h, G), RS_ERR_ARG,
              "RS_PC_FORM=tc:%d needs float32, TH a multiple of %d (at most %d chunks), X and Y multiples of %d "
              "and >= %d, at most %d path filters", G, G, TC_NCH_MAX, TC_T, TC_UW, RT_NFMAX);
+    // the path kernel's union image is dynamic LDS, up to TC_UW rows
+#define PC_TC_ATTR(g_, nw_)                                                                                  \
+    if (G == g_ && nw == nw_)                                                                                \
+        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_path_tc<g_, nw_>),                     \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tc_union_lds_bytes(g_, TC_UW)));
+    PC_TC_VARIANTS(PC_TC_ATTR)
+#undef PC_TC_ATTR
     h->streamed = false;
     h->cols = true;
     h->halo = false;

@@ -76,8 +76,15 @@ def main():
         child(shape, a.calls, a.loop_so, a.mode)
         return
     so = build_loop() if a.mode == 'anatomy' else ''
-    for form in a.forms:
+    for spec in a.forms:
+        # FORM[@VAR=V,...]: e.g. halo@ROC_ACTIVE_WAIT_TIMEOUT=100 (the HIP runtime's host
+        # spin before it sleeps on the completion interrupt)
+        form, _, extra = spec.partition('@')
         env = dict(os.environ, RS_PC_FORM=form)
+        for kv in filter(None, extra.split(',')):
+            k, v = kv.split('=', 1)
+            env[k] = v
+        print('#', spec, flush=True)
         subprocess.check_call([sys.executable, os.path.abspath(__file__), '--child', '--shape', a.shape,
                                '--calls', str(a.calls), '--loop-so', so, '--mode', a.mode], env=env)
 

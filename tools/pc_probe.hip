@@ -79,7 +79,8 @@ int main(int argc, char** argv) {
     }
     rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
     unsigned long long* dbg;
-    const size_t ndbg = 8 * 4096 * 8;
+    constexpr int NKID = 16;  // stamp slots: kernel id x 4096 blocks x 8 stamps
+    const size_t ndbg = (size_t)NKID * 4096 * 8;
     CK(hipMalloc(&dbg, ndbg * 8));
     CK(hipMemset(dbg, 0, ndbg * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(pc_dbg), &dbg, sizeof(dbg)));
@@ -111,51 +112,69 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> st(ndbg);
     CK(hipMemcpy(st.data(), dbg, ndbg * 8, hipMemcpyDeviceToHost));
     const int nb = h->nPart;
-    static const char* kname[8] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
-                                   "excite_cols", "path_cols", "halo"};
-    static const int kns[8] = {4, 6, 5, 5, 0, 5, 5, 7};
-    for (int kid = 0; kid < 8; ++kid) {
-        if (kid == 4) continue;  // shader-clock stamps, below
+    auto slot = [&](int kid, int b, int i) { return st[((size_t)kid * 4096 + b) * 8 + i]; };
+    // only the kernels of this handle's form, and of those only the stamps every block
+    // wrote: a slot no block stamped (a phase this build does not stamp) is reported as
+    // such, never as a difference against zero
+    static const char* kname[NKID] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
+                                      "excite_cols", "path_cols", "halo", "excite_tc", "path_tc"};
+    static const int kns[NKID] = {4, 6, 5, 5, 0, 5, 5, 7, 5, 4};
+    std::vector<int> kids;
+    if (h->halo) kids = {7};
+    else if (h->tcG > 0) kids = {8, 9};
+    else if (h->cols) kids = {5, 6};
+    else if (h->streamed) kids = {2, 3};
+    else if (h->tiling) kids = {0, 1};
+    auto stamped = [&](int kid, int i) {
+        for (int b = 0; b < nb; ++b)
+            if (slot(kid, b, i) == 0) return false;
+        return true;
+    };
+    for (int kid : kids) {
         const int ns = kns[kid];
-        if (st[(size_t)kid * 4096 * 8] == 0) continue;  // kernel not used by this step form
-        unsigned long long t0 = ~0ull, t1 = 0;
-        std::vector<std::vector<double>> ph(ns);
-        for (int b = 0; b < nb; ++b) {
-            const unsigned long long* r = &st[((size_t)kid * 4096 + b) * 8];
-            t0 = std::min(t0, r[0]);
-            t1 = std::max(t1, r[ns - 1]);
-            for (int i = 1; i < ns; ++i) ph[i].push_back((r[i] - r[i - 1]) * 10.0);
-            ph[0].push_back((double)r[0]);
+        if (!stamped(kid, 0) || !stamped(kid, ns - 1)) {
+            printf("%s: start/end not stamped by this build\n", kname[kid]);
+            continue;
         }
+        unsigned long long t0 = ~0ull, t1 = 0;
         std::vector<double> starts;
-        for (int b = 0; b < nb; ++b) starts.push_back((st[((size_t)kid * 4096 + b) * 8] - t0) * 10.0);
+        for (int b = 0; b < nb; ++b) {
+            t0 = std::min(t0, slot(kid, b, 0));
+            t1 = std::max(t1, slot(kid, b, ns - 1));
+        }
+        for (int b = 0; b < nb; ++b) starts.push_back((slot(kid, b, 0) - t0) * 10.0);
         printf("%s: first start -> last end %.2f us; start spread median %.2f max %.2f us\n",
                kname[kid], (t1 - t0) * 1e-2, median(starts) * 1e-3,
                *std::max_element(starts.begin(), starts.end()) * 1e-3);
-        for (int i = 1; i < ns; ++i)
-            printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph[i]) * 1e-3,
-                   *std::max_element(ph[i].begin(), ph[i].end()) * 1e-3);
+        for (int i = 1; i < ns; ++i) {
+            if (!stamped(kid, i - 1) || !stamped(kid, i)) {
+                printf("   phase %d: not stamped\n", i);
+                continue;
+            }
+            std::vector<double> ph;
+            for (int b = 0; b < nb; ++b) ph.push_back((double)(slot(kid, b, i) - slot(kid, b, i - 1)) * 10.0);
+            printf("   phase %d: median %.2f us  max %.2f us\n", i, median(ph) * 1e-3,
+                   *std::max_element(ph.begin(), ph.end()) * 1e-3);
+        }
     }
     // the last step's kernel boundary: excitation's last block end -> path's first block start
-    for (int ek = 0; ek < 7; ek += 5) {  // (0, 1) rows, (5, 6) cols
-        const int pk = ek + 1;
-        if (st[(size_t)ek * 4096 * 8] == 0 || st[(size_t)pk * 4096 * 8] == 0) continue;
+    if (kids.size() == 2 && stamped(kids[0], kns[kids[0]] - 1) && stamped(kids[1], 0)) {
+        const int ek = kids[0], pk = kids[1];
         unsigned long long e1 = 0, p0 = ~0ull, e0 = ~0ull, p1 = 0;
         for (int b = 0; b < nb; ++b) {
-            const unsigned long long* re = &st[((size_t)ek * 4096 + b) * 8];
-            const unsigned long long* rp = &st[((size_t)pk * 4096 + b) * 8];
-            e0 = std::min(e0, re[0]);
-            e1 = std::max(e1, re[kns[ek] - 1]);
-            p0 = std::min(p0, rp[0]);
-            p1 = std::max(p1, rp[kns[pk] - 1]);
+            e0 = std::min(e0, slot(ek, b, 0));
+            e1 = std::max(e1, slot(ek, b, kns[ek] - 1));
+            p0 = std::min(p0, slot(pk, b, 0));
+            p1 = std::max(p1, slot(pk, b, kns[pk] - 1));
         }
         printf("boundary %s -> %s: %.2f us (excite first start -> path last end %.2f us)\n", kname[ek],
                kname[pk], ((double)p0 - (double)e1) * 1e-2, ((double)p1 - (double)e0) * 1e-2);
     }
-    if (h->halo && st[(size_t)4 * 4096 * 8] != 0) {  // the halo kernel's theta pass (stamps 4, 0..1)
+    if (h->halo && stamped(11, 0) && stamped(11, 1) && stamped(10, 0) && stamped(10, 1) && stamped(7, 1)) {
+        // the halo kernel's phase-1 DMA (stamps 10, 0..1) and theta pass (11, 0..1)
         std::vector<double> a, b;
         for (int bb = 0; bb < h->nPart; ++bb) {
-            const unsigned long long* r4 = &st[((size_t)4 * 4096 + bb) * 8];
+            const unsigned long long* r4 = &st[((size_t)11 * 4096 + bb) * 8];
             const unsigned long long* r7 = &st[((size_t)7 * 4096 + bb) * 8];
             a.push_back((double)(r4[0] - r7[1]) * 10.0);
             b.push_back((double)(r4[1] - r4[0]) * 10.0);
@@ -165,7 +184,7 @@ int main(int argc, char** argv) {
         {
             std::vector<double> i1, w1;
             for (int bb = 0; bb < h->nPart; ++bb) {
-                const unsigned long long* r3 = &st[((size_t)3 * 4096 + bb) * 8];
+                const unsigned long long* r3 = &st[((size_t)10 * 4096 + bb) * 8];
                 const unsigned long long* r7 = &st[((size_t)7 * 4096 + bb) * 8];
                 i1.push_back((double)(r3[0] - r7[0]) * 10.0);
                 w1.push_back((double)(r3[1] - r7[0]) * 10.0);
@@ -176,23 +195,16 @@ int main(int argc, char** argv) {
         printf("   halo phase 2 per wave, task loop end after phase 1 (median us):");
         for (int w = 0; w < 9; ++w) {
             std::vector<double> c;
+            if (!stamped(12 + w / 8, w % 8)) {
+                printf(" -");
+                continue;
+            }
             for (int bb = 0; bb < h->nPart; ++bb)
-                c.push_back((double)(st[((size_t)(5 + w / 8) * 4096 + bb) * 8 + w % 8] -
+                c.push_back((double)(st[((size_t)(12 + w / 8) * 4096 + bb) * 8 + w % 8] -
                                      st[((size_t)7 * 4096 + bb) * 8 + 1]) * 10.0);
             printf(" %.2f", median(c) * 1e-3);
         }
         printf("\n");
-    } else if (st[(size_t)4 * 4096 * 8] != 0) {  // shader-clock phases of layer 5 (excite stream)
-        const char* nm[6] = {"vmcnt wait", "lds store+prefetch+barrier", "y pass", "barrier 2",
-                             "x pass", "theta pass"};
-        for (int i = 1; i < 7; ++i) {
-            std::vector<double> c;
-            for (int b = 0; b < h->nPart; ++b) {
-                const unsigned long long* r = &st[((size_t)4 * 4096 + b) * 8];
-                c.push_back((double)(r[i] - r[i - 1]));
-            }
-            printf("   excite layer-5 %-28s median %6.0f cycles\n", nm[i - 1], median(c));
-        }
     }
     if (h->halo) {  // back-to-back launch cost of the halo kernel alone, and of an empty one
         hipEvent_t c0, c1;
@@ -219,6 +231,37 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
         printf("halo step alone: %.2f us/launch\n", 1e3 * t / reps);
+        rs_pc_destroy(h);
+        return 0;
+    }
+    if (h->tcG > 0) {  // back-to-back launch costs of the theta-chunked kernels
+        hipEvent_t c0, c1;
+        CK(hipEventCreate(&c0));
+        CK(hipEventCreate(&c1));
+        const dim3 g(h->cgx * h->cgy * h->coNch), b(64 * h->tcNW);
+        const int reps = 500;
+        float t = 0;
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(empty_kernel, g, b, 0, h->stream, nullptr);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
+        PcCtlTc c;
+        make_ctl_tc(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
+        const StepOut so = step_out(h, 0);
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i) pc_launch_tc(h, so, nullptr, -1);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
+        CK(hipEventRecord(c0, h->stream));
+        for (int i = 0; i < reps; ++i) pc_launch_tc(h, so, &c, -1);
+        CK(hipEventRecord(c1, h->stream));
+        CK(hipEventSynchronize(c1));
+        CK(hipEventElapsedTime(&t, c0, c1));
+        printf("excite + path: %.2f us/step\n", 1e3 * t / reps);
         rs_pc_destroy(h);
         return 0;
     }
