@@ -2519,7 +2519,7 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     int n4, const double* __restrict__ part,
     int npart, unsigned long long* __restrict__ slot, const unsigned long long* __restrict__ res,
     int nexp, unsigned* __restrict__ counter, unsigned long long* __restrict__ host,
-    double* __restrict__ xp, int nbytes) {
+    double* __restrict__ xp, int nbytes, int fence) {
     __shared__ unsigned long long s_bk[4];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2549,15 +2549,20 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
         if (slot) atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
         s_last = 0;
         if (nexp > 0) {
-            // the key has reached memory (agent-scope atomics execute there) before
-            // this block counts itself done: an agent-scope release orders it before
-            // the counter add (and the wait covers the write-back the fence issues)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            // The hand-off of the keys to the block that counts last: the key is an
+            // agent-scope atomic (performed at memory, never held in an L2), each block's
+            // one lane waits for it (vmcnt(0)) before its counter add, the last adder
+            // learns it from the value its add returns, and it reads the slots with sc1
+            // loads only -- the hand-off MI355X_MICROARCH.md measures valid without an
+            // acquire ("Hand-offs measured with sc1 loads in place of the acquire", first
+            // row; not an architectural guarantee).  fence = 1 adds the model's agent
+            // release / acquire pair (RS_PC_HALO_FENCE=1): a buffer_wbl2 in every block,
+            // +1.5 us per update() at 64x64x36 (tools/pc_call_anatomy.py, round 5).
+            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                      gridDim.x - 1;
-            // the block that counts last acquires every other block's released keys
-            if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (fence && s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
     }
     __syncthreads();
@@ -2616,10 +2621,9 @@ struct PcCtlTc {
 };
 
 // Dynamic LDS of the chunked path kernel for a union of `rows` rows: whole rows of
-// TC_UW cells of 4 (G/4 + 2) floats, plus one wave-instruction of slack for the last
-// LDS-DMA pieces.
+// TC_UW cells of 4 (G/4 + 2) floats (LDS-DMA pieces past the image are masked off).
 inline size_t tc_union_lds_bytes(int G, int rows) {
-    return ((size_t)rows * TC_UW * 4 * (G / 4 + 2) + 64 * 4) * sizeof(float);
+    return (size_t)rows * TC_UW * 4 * (G / 4 + 2) * sizeof(float);
 }
 
 template <int G>
@@ -2670,14 +2674,28 @@ __device__ inline void tc_window_dma(const float* __restrict__ src, float* s, in
     }
 }
 
-// The normalisation total from the per-block partials in one fixed order (lane-strided,
-// then DPP): the same bits in every wave of every block.
-__device__ inline double tc_partials_total(const double* __restrict__ part, int npart) {
-    const int lane = threadIdx.x & 63;
-    double t = 0.0;
-    for (int i = lane; i < npart; i += 64) t += part[i];
-    return co_wave_sum(t);
-}
+// The normalisation total from the per-block partials in one fixed order (lane-strided
+// in increasing index, then DPP): the same bits in every wave of every block.  The first
+// 64 * TC_NPL partials are loaded by issue(), all in flight together, so that their
+// round trip overlaps the window's (one load in flight at a time: 12 serial round trips
+// to memory, ~5 us, at 768 blocks); sum() adds them and any beyond.
+constexpr int TC_NPL = 16;
+struct TcPartials {
+    double v[TC_NPL];
+    __device__ inline void issue(const double* __restrict__ part, int npart) {
+        const int lane = threadIdx.x & 63, last = npart > 0 ? npart - 1 : 0;
+#pragma unroll
+        for (int u = 0; u < TC_NPL; ++u) v[u] = part[min(lane + 64 * u, last)];
+    }
+    __device__ inline double sum(const double* __restrict__ part, int npart) const {
+        const int lane = threadIdx.x & 63;
+        double t = 0.0;
+#pragma unroll
+        for (int u = 0; u < TC_NPL; ++u) t += lane + 64 * u < npart ? v[u] : 0.0;
+        for (int i = lane + 64 * TC_NPL; i < npart; i += 64) t += part[i];
+        return co_wave_sum(t);
+    }
+};
 
 // Excitation (posecell_network.py:336 -> convolution.py:228-246) + inhibition
 // (:339-340) + the block's partial of the normalisation total (:343) for one chunk:
@@ -2693,7 +2711,8 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_tc(const float* __restrict_
     constexpr int WIN = TC_W * TC_W * LU;                 // window image [cell][local layer]
     constexpr int XB = 2 * TC_T * TC_T * LU;              // x-pass outputs (e | i) [cell][L], aliasing the window
     static_assert(XB <= WIN, "x-pass outputs fit the dead window");
-    __shared__ __attribute__((aligned(16))) float s_w[WIN + 64 * 4];
+    // (no slack after the window: a wave-instruction's pieces past the window are masked off)
+    __shared__ __attribute__((aligned(16))) float s_w[WIN];
     __shared__ __attribute__((aligned(16))) float s_y[2 * TC_W * TC_T * YP];  // y-pass outputs (e | i) [r][c][L]
     __shared__ double s_red[NW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2840,6 +2859,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_tc(const float* __restrict__ 
     const TcTile tl = tc_tile(nblk, gx, nch);
     const int k0 = tl.ch * G;
     PC_STAMP(9, 0);
+    // wave 0: the normalisation partials' loads first (summed after the window's issue)
+    TcPartials pt;
+    if (wave == 0) pt.issue(part, npart);
     // 1. the union of the chunk's layers' shifted 14 x 14 windows (host-formed)
     const int uorg = ctl.uorg[tl.ch], uext = ctl.uext[tl.ch];
     const int umx = (short)(uorg & 0xFFFF), umy = uorg >> 16, UW = uext & 0xFFFF, UH = uext >> 16;
@@ -2864,7 +2886,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_tc(const float* __restrict__ 
     }
     for (int i = tid; i < nf * FT; i += NT) s_ftab[(i / FT) * ST_FTP + i % FT] = filt[i];
     if (wave == 0) {
-        const double t = tc_partials_total(part, npart);
+        const double t = pt.sum(part, npart);
         if (lane == 0) s_tot = t;
     }
     if (uni) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces have landed
@@ -3511,14 +3533,24 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         RS_HIP(hipGetLastError());
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
     }
-    const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX;
+    // RS_PC_HALO_EXPORT=kernel: the keys exported by a pc_res_export launch instead of
+    // the finishing kernel's last block (A/B); RS_PC_HALO_FENCE=1: the hand-off fenced
+    static const bool export_kernel = [] {
+        const char* e = std::getenv("RS_PC_HALO_EXPORT");
+        return e && std::strcmp(e, "kernel") == 0;
+    }();
+    static const int fence = [] {
+        const char* e = std::getenv("RS_PC_HALO_FENCE");
+        return e && std::strcmp(e, "1") == 0 ? 1 : 0;
+    }();
+    const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX && !export_kernel;
     const int n4 = (int)(h->n / 4);
     const int nb = std::min(1024, (n4 + 255) / 256);
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
     hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[n & 1], buf[0], n4,
                        h->dPart + (size_t)((n - 1) & 1) * h->nPart, h->nPart,
                        h->dRes + (size_t)(n - 1) * RES_SLOTS, h->dRes, own_export ? n : 0, h->dCounter,
-                       h->hResDev, h->exportDev, (int)(h->n * sizeof(float)));
+                       h->hResDev, h->exportDev, (int)(h->n * sizeof(float)), fence);
     RS_HIP(hipGetLastError());
     if (!h->dbgSkipExport && !own_export) {
         hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,

@@ -3,7 +3,7 @@
 
 usage: python tools/pc_ab.py LIB.so[@ENV=V,...] [LIB2.so ...] [--shape 128,128,72] [--steps 2000] [--rounds 3]
        [--mode run|update|node]
-(``@RS_PC_CTL=inline`` runs that library with the variable set)
+(``@RS_PC_CTL=inline`` runs that library with the variable set; ``;`` separates several)
 Each library runs in its own process (ctypes loads one copy), interleaved over
 rounds so clock drift hits every build alike: batched run() steps/s after a clock
 warm-up, and the state after the same odometry, compared across builds.  A build
@@ -86,7 +86,8 @@ def main():
         for i, lib in enumerate(a.libs):
             out = '/tmp/pc_ab_%d.npy' % i
             path, _, envs = lib.partition('@')
-            env = dict(os.environ, **dict(kv.split('=', 1) for kv in envs.split(',') if kv))
+            # LIB@K=V;K2=V2 (';' between variables: a value may hold commas, tc:24,4)
+            env = dict(os.environ, **dict(kv.split('=', 1) for kv in envs.split(';') if kv))
             p = subprocess.run([sys.executable, __file__, path, '--child', '--shape', a.shape, '--steps',
                                 str(a.steps), '--check', str(a.check), '--precision', a.precision,
                                 '--out', out, '--mode', a.mode], capture_output=True, text=True, timeout=300, env=env)

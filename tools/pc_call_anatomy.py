@@ -77,11 +77,11 @@ def main():
         return
     so = build_loop() if a.mode == 'anatomy' else ''
     for spec in a.forms:
-        # FORM[@VAR=V,...]: e.g. halo@ROC_ACTIVE_WAIT_TIMEOUT=100 (the HIP runtime's host
+        # FORM[@VAR=V;...]: e.g. halo@ROC_ACTIVE_WAIT_TIMEOUT=100 (the HIP runtime's host
         # spin before it sleeps on the completion interrupt)
         form, _, extra = spec.partition('@')
         env = dict(os.environ, RS_PC_FORM=form)
-        for kv in filter(None, extra.split(',')):
+        for kv in filter(None, extra.split(';')):
             k, v = kv.split('=', 1)
             env[k] = v
         print('#', spec, flush=True)
