@@ -3244,7 +3244,8 @@ struct rs_pc {
                             // P and Q are then theta-fastest (C order (x, y, th))
     bool halo = false;      // one launch per step (RS_PC_FORM=halo): HF_T x HF_T tiles through all
                             // layers, the excitation recomputed on each tile's halo; P theta-fastest
-    int tcG = 0, tcNW = 4;  // theta-chunked column kernels (RS_PC_FORM=tc[:G[,NW]]; cols is set too:
+    bool tcExcCols = false;  // tc: the cols form's whole-extent excitation kernel (RS_PC_FORM=tc:G,NW,1)
+    int tcG = 0, tcNW = 4;  // theta-chunked column kernels (RS_PC_FORM=tc[:G[,NW[,E]]]; cols is set too:
                             // theta-fastest P and Q, cgx x cgy tiles of TC_T, coNch = TH / G chunks)
     unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
     int cgx = 0, cgy = 0;   // column (or halo) tiles along x and y
@@ -3462,7 +3463,7 @@ void make_ctl_tc(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, co
 }
 
 // The instantiated (G, NW) pairs of the theta-chunked kernels.
-#define PC_TC_VARIANTS(X_) X_(12, 4) X_(24, 4) X_(24, 8) X_(36, 8)
+#define PC_TC_VARIANTS(X_) X_(12, 4) X_(24, 4) X_(24, 8) X_(36, 4) X_(36, 8)
 
 // One step of the theta-chunked form: the excitation, then (ctl != nullptr) the path kernel.
 int pc_launch_tc(rs_pc* h, const StepOut& so, const PcCtlTc* ctl, int prof_base) {
@@ -3471,6 +3472,13 @@ int pc_launch_tc(rs_pc* h, const StepOut& so, const PcCtlTc* ctl, int prof_base)
     float* Q = static_cast<float*>(h->dQ);
     bool done = false;
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
+    if (h->tcExcCols) {   // the whole-extent column excitation, one block per 8 x 8 tile
+        const dim3 ge(h->cgx * h->cgy);
+        hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, CO_DMA_TH>), ge,
+                           dim3(64 * CO_NW), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, h->cgy, (int)ge.x, Q,
+                           h->dPart, so.slot, h->TH, h->kf);
+        done = true;
+    }
 #define PC_TC_EXC(g_, nw_)                                                                                      \
     if (!done && h->tcG == g_ && h->tcNW == nw_) {                                                            \
         hipLaunchKernelGGL((pc_excite_tc<g_, nw_>), g, dim3(64 * nw_), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, \
@@ -4057,9 +4065,13 @@ int pc_choose_form(rs_pc* h) {
         return pc_halo_set(h);
     }
     if (env && (std::strcmp(env, "tc") == 0 || std::strncmp(env, "tc:", 3) == 0)) {
-        int G = 24, nw = 4;
-        if (env[2] == ':') std::sscanf(env + 3, "%d,%d", &G, &nw);
-        return pc_tc_set(h, G, nw);
+        int G = 24, nw = 4, ec = 0;
+        if (env[2] == ':') std::sscanf(env + 3, "%d,%d,%d", &G, &nw, &ec);
+        RS_TRY(pc_tc_set(h, G, nw));
+        RS_CHECK(!ec || (h->TH == CO_DMA_TH && CO_TX == TC_T && CO_TY == TC_T), RS_ERR_ARG,
+                 "RS_PC_FORM=tc:G,NW,1 (the cols excitation) needs TH == %d", CO_DMA_TH);
+        h->tcExcCols = ec != 0;
+        return RS_OK;
     }
     if (env && std::strcmp(env, "rows") == 0) {
         RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=rows needs Y <= 128");
@@ -4190,8 +4202,9 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         h->nPart = h->cgx * h->cgy;
         h->nPathBlocks = h->nPart;
     } else if (h->cols) {
-        h->nPart = h->cgx * h->cgy * h->coNch;
-        h->nPathBlocks = h->nPart;
+        h->nPathBlocks = h->cgx * h->cgy * h->coNch;
+        // (tc with the cols excitation: one excitation block per 8 x 8 tile, all layers)
+        h->nPart = h->tcExcCols ? h->cgx * h->cgy : h->nPathBlocks;
     } else if (h->streamed) {
         h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;
         h->nPathBlocks = h->nPart;

@@ -11,7 +11,7 @@ from oracle import posecell as P
 pytestmark = pytest.mark.gpu
 
 F32_TOL = 1e-5
-VARIANTS = ['tc:12,4', 'tc:24,4', 'tc:24,8', 'tc:36,8']
+VARIANTS = ['tc:12,4', 'tc:24,4', 'tc:24,8', 'tc:36,4', 'tc:36,8', 'tc:24,4,1', 'tc:36,8,1']
 
 
 @pytest.fixture(scope='module')
@@ -29,8 +29,11 @@ def odometry(n, seed, vmax=0.6, rmax=0.15):
 
 def fits(shape, form):
     X, Y, TH = shape
-    G = int(form.split(':')[1].split(',')[0])
-    return X % 8 == 0 and Y % 8 == 0 and X >= 20 and Y >= 20 and TH % G == 0 and TH // G <= 18
+    parts = [int(p) for p in form.split(':')[1].split(',')]
+    G = parts[0]
+    cols_exc = len(parts) > 2 and parts[2] == 1        # the cols excitation: TH == 72 only
+    return (X % 8 == 0 and Y % 8 == 0 and X >= 20 and Y >= 20 and TH % G == 0 and TH // G <= 18 and
+            (not cols_exc or TH == 72))
 
 
 @pytest.mark.parametrize('form', VARIANTS)
