@@ -2582,420 +2582,6 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     }
 }
 
-// ---------------------------------------------------------------------------
-// Theta-chunked column form (float32, theta-fastest P and Q, TH % 4 == 0): the two
-// kernels of a step, each cut into many small blocks that several share a CU.
-//
-// A block owns an 8 x 8 tile of cells through a chunk of G layers (TH / G chunks).
-// The reference's step (posecell_network.py:326-353) couples layers only through the
-// two 7-tap theta passes (the excitation's, convolution.py:228-246, and conv_z,
-// :344-359), so a chunk needs 3 halo layers each side; the xy passes need 3 halo cells
-// (excitation) and 3 plus the layer's shift (the path filter, :320-340).  With the
-// whole theta extent in one block (the cols form) a CU held one block of 12 waves and
-// ran its phases in lockstep: loads, then LDS passes, each latency-bound.
-// Here 2-4 blocks share a CU at different phases, and the path kernel's window is the
-// union of G + 6 layers' shifted windows, not of all TH layers'.
-//  * Every 16-byte unit of a cell's theta column (4 layers, theta-fastest) is one
-//    LDS-DMA piece; a block loads NU = G/4 + 2 units per cell: layers k0-4 .. k0+G+3
-//    (k0 = chunk * G, a multiple of 4), of which it uses k0-3 .. k0+G+2.
-//  * The window image is [cell][unit] (a cell's 4 NU local layers contiguous, local
-//    layer l = global k0 - 4 + l): lanes on consecutive layers of a task read
-//    consecutive words (conflict-free), and a thread's window reads take immediate
-//    offsets.
-// ---------------------------------------------------------------------------
-constexpr int TC_T = 8;                    // tile: TC_T x TC_T cells
-constexpr int TC_W = TC_T + 2 * HALF;      // 14: the excitation window, the path window per layer
-constexpr int TC_MS = 6;                   // the path kernel's union: layers' centred shifts spread <= 6
-constexpr int TC_UW = TC_W + TC_MS;        // 20: union rows / columns held in LDS
-constexpr int TC_NCH_MAX = 18;             // chunks per step (TH / G)
-
-// One step's control for the chunked path kernel (a kernel argument, ~0.6 KiB).
-struct PcCtlTc {
-    short iox[CTL_INLINE_MAX], ioy[CTL_INLINE_MAX];  // per-layer shifts (centred on the host)
-    unsigned char ifi[CTL_INLINE_MAX];               // per-layer path filter row
-    float zf[FL];                                    // theta filter (posecell_network.py:308)
-    // chunk c's union of its G + 6 layers' shifted windows: origin (smallest centred
-    // shift) and extent, packed as 16-bit pairs (lo: x, hi: y)
-    int uorg[TC_NCH_MAX], uext[TC_NCH_MAX];
-    int urows;   // union rows held in LDS by this launch (the widest fitting chunk's UW)
-};
-
-// Dynamic LDS of the chunked path kernel for a union of `rows` rows: whole rows of
-// TC_UW cells of 4 (G/4 + 2) floats (LDS-DMA pieces past the image are masked off).
-inline size_t tc_union_lds_bytes(int G, int rows) {
-    return (size_t)rows * TC_UW * 4 * (G / 4 + 2) * sizeof(float);
-}
-
-template <int G>
-struct TcGeom {
-    static constexpr int NU = G / 4 + 2;   // 16-byte units loaded per cell
-    static constexpr int LU = 4 * NU;      // local layers per cell in LDS
-    static constexpr int NL = G + 2 * HALF;  // layers a chunk computes the 2-D passes for
-    static_assert(G % 4 == 0 && G >= 4, "chunks of whole 16-byte units");
-};
-
-// The chunk's tile from the block index: tiles are numbered chunk-fastest and dealt to
-// the XCDs in consecutive runs (st_tile), so an XCD holds whole rows of tiles with all
-// their chunks and its L2 serves the halos and the chunks' shared units.
-struct TcTile {
-    int x0, y0, ch;
-};
-__device__ inline TcTile tc_tile(int nblk, int gx, int nch) {
-    const int t = st_tile(blockIdx.x, nblk), xy = t / nch;
-    return TcTile{(xy % gx) * TC_T, (xy / gx) * TC_T, t - xy * nch};
-}
-
-// Issue the LDS-DMA of a window of nr x nc cells (row pitch RP cells in LDS, columns
-// nc .. RP-1 not loaded) starting at cell (gx0, gy0) (wrapped), NU units per cell from
-// unit u0 of the theta column (wrapped mod TH/4).  Piece p = (r * RP + c) * NU + u lands
-// at s + 4p.  Returns nothing; the caller waits vmcnt(0) before its barrier.
-template <int NU, int RP, int NR, int NTH>
-__device__ inline void tc_window_dma(const float* __restrict__ src, float* s, int X, int Y, int TH, int gx0,
-                                     int gy0, int u0, int nr, int nc) {
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int th4 = TH >> 2, npc = nr * RP * NU;
-    constexpr int NK = (NR * RP * NU + NTH - 1) / NTH;
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-        const int i0 = k * NTH + wave * 64;  // wave-uniform
-        if (i0 < npc) {
-            const int p = i0 + lane, c = p / NU, u = p - c * NU, r = c / RP, cc = c - r * RP;
-            if (p < npc && cc < nc) {
-                int gr = gx0 + r, gc = gy0 + cc, gu = u0 + u;
-                gr -= gr >= X ? X : 0;
-                gc -= gc >= Y ? Y : 0;
-                gu -= gu >= th4 ? th4 : 0;
-                const unsigned off = ((unsigned)gr * Y + gc) * TH + 4 * gu;   // n * 4 <= INT_MAX
-                __builtin_amdgcn_global_load_lds(
-                    (__attribute__((address_space(1))) const void*)(src + off),
-                    (__attribute__((address_space(3))) void*)(s + 4 * i0), 16, 0, 0);
-            }
-        }
-    }
-}
-
-// The normalisation total from the per-block partials in one fixed order (lane-strided
-// in increasing index, then DPP): the same bits in every wave of every block.  The first
-// 64 * TC_NPL partials are loaded by issue(), all in flight together, so that their
-// round trip overlaps the window's (one load in flight at a time: 12 serial round trips
-// to memory, ~5 us, at 768 blocks); sum() adds them and any beyond.
-constexpr int TC_NPL = 16;
-struct TcPartials {
-    double v[TC_NPL];
-    __device__ inline void issue(const double* __restrict__ part, int npart) {
-        const int lane = threadIdx.x & 63, last = npart > 0 ? npart - 1 : 0;
-#pragma unroll
-        for (int u = 0; u < TC_NPL; ++u) v[u] = part[min(lane + 64 * u, last)];
-    }
-    __device__ inline double sum(const double* __restrict__ part, int npart) const {
-        const int lane = threadIdx.x & 63;
-        double t = 0.0;
-#pragma unroll
-        for (int u = 0; u < TC_NPL; ++u) t += lane + 64 * u < npart ? v[u] : 0.0;
-        for (int i = lane + 64 * TC_NPL; i < npart; i += 64) t += part[i];
-        return co_wave_sum(t);
-    }
-};
-
-// Excitation (posecell_network.py:336 -> convolution.py:228-246) + inhibition
-// (:339-340) + the block's partial of the normalisation total (:343) for one chunk:
-// y pass and x pass on the chunk's G + 6 layers, then the theta pass to its G layers.
-template <int G, int NW>
-__global__ __launch_bounds__(64 * NW) void pc_excite_tc(const float* __restrict__ P, int X, int Y, int TH, int gx,
-                                                        int nch, int nblk, float* __restrict__ Q,
-                                                        double* __restrict__ part,
-                                                        unsigned long long* __restrict__ res_slot,
-                                                        SepKernel<float> k) {
-    using Gm = TcGeom<G>;
-    constexpr int NT = 64 * NW, NU = Gm::NU, LU = Gm::LU, NL = Gm::NL, YP = NL + 1;
-    constexpr int WIN = TC_W * TC_W * LU;                 // window image [cell][local layer]
-    constexpr int XB = 2 * TC_T * TC_T * LU;              // x-pass outputs (e | i) [cell][L], aliasing the window
-    static_assert(XB <= WIN, "x-pass outputs fit the dead window");
-    // (no slack after the window: a wave-instruction's pieces past the window are masked off)
-    __shared__ __attribute__((aligned(16))) float s_w[WIN];
-    __shared__ __attribute__((aligned(16))) float s_y[2 * TC_W * TC_T * YP];  // y-pass outputs (e | i) [r][c][L]
-    __shared__ double s_red[NW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TcTile tl = tc_tile(nblk, gx, nch);
-    const int k0 = tl.ch * G;
-    PC_STAMP(8, 0);
-    // 1. the 14 x 14-cell window, NU units per cell (layers k0-4 .. k0+G+3)
-    {
-        int gx0 = tl.x0 - HALF, gy0 = tl.y0 - HALF, u0 = (k0 >> 2) - 1;
-        gx0 += gx0 < 0 ? X : 0;
-        gy0 += gy0 < 0 ? Y : 0;
-        u0 += u0 < 0 ? (TH >> 2) : 0;
-        tc_window_dma<NU, TC_W, TC_W, NT>(P, s_w, X, Y, TH, gx0, gy0, u0, TC_W, TC_W);
-    }
-    if (res_slot != nullptr && blockIdx.x == 0)
-        for (int i = tid; i < RES_SLOTS; i += NT) st_wt(&res_slot[i], 0ull);  // the path kernel max-reduces into them
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces have landed
-    co_lds_barrier();
-    PC_STAMP(8, 1);
-    // 2. y pass: task (window row r, layer L) -> TC_T outputs of each Gaussian from the
-    //    row's 14 cells (local layer 1 + L = global k0 - 3 + L)
-    float* s_ye = s_y;
-    float* s_yi = s_y + TC_W * TC_T * YP;
-    for (int t = tid; t < TC_W * NL; t += NT) {
-        const int r = t / NL, L = t - r * NL;
-        const float* row = s_w + r * TC_W * LU + 1 + L;
-        float w[TC_W];
-#pragma unroll
-        for (int c = 0; c < TC_W; ++c) w[c] = row[c * LU];
-#pragma unroll
-        for (int c = 0; c < TC_T; ++c) {
-            float e = 0.f, g = 0.f;
-#pragma unroll
-            for (int q = 0; q < FL; ++q) {
-                e += k.ge[q] * w[c + q];
-                g += k.gi[q] * w[c + q];
-            }
-            s_ye[(r * TC_T + c) * YP + L] = e;
-            s_yi[(r * TC_T + c) * YP + L] = g;
-        }
-    }
-    co_lds_barrier();
-    PC_STAMP(8, 2);
-    // 3. x pass: task (column c, layer L) -> TC_T outputs from the 14 y-pass rows, into
-    //    [cell][L] rows of pitch LU (16-byte aligned: the theta pass reads vectors)
-    float* s_xe = s_w;
-    float* s_xi = s_w + TC_T * TC_T * LU;
-    for (int t = tid; t < TC_T * NL; t += NT) {
-        const int c = t / NL, L = t - c * NL;
-        float ye[TC_W], yi[TC_W];
-#pragma unroll
-        for (int a = 0; a < TC_W; ++a) {
-            ye[a] = s_ye[(a * TC_T + c) * YP + L];
-            yi[a] = s_yi[(a * TC_T + c) * YP + L];
-        }
-#pragma unroll
-        for (int i = 0; i < TC_T; ++i) {
-            float e = 0.f, g = 0.f;
-#pragma unroll
-            for (int q = 0; q < FL; ++q) {
-                e += k.ge[q] * ye[i + q];
-                g += k.gi[q] * yi[i + q];
-            }
-            s_xe[(i * TC_T + c) * LU + L] = e;
-            s_xi[(i * TC_T + c) * LU + L] = g;
-        }
-    }
-    co_lds_barrier();
-    PC_STAMP(8, 3);
-    // 4. theta pass + inhibition: task (cell p, group j of 4 output layers): output o =
-    //    4j + d (global k0 + o) takes L = o .. o + 6; one 16-byte write-through store
-    double sum = 0.f;
-    {
-        constexpr int NG = G / 4;
-        const int nbytes = (int)min((size_t)X * Y * TH * sizeof(float), (size_t)INT_MAX);
-        for (int t = tid; t < TC_T * TC_T * NG; t += NT) {
-            const int p = t / NG, j = t - p * NG;
-            const co_f4* se = reinterpret_cast<const co_f4*>(s_xe + p * LU + 4 * j);
-            const co_f4* si = reinterpret_cast<const co_f4*>(s_xi + p * LU + 4 * j);
-            float re[12], ri[12];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const co_f4 a = se[q], b = si[q];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    re[4 * q + c] = a[c];
-                    ri[4 * q + c] = b[c];
-                }
-            }
-            co_f4 qv;
-#pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                float e = 0.f, g = 0.f;
-#pragma unroll
-                for (int z = 0; z < FL; ++z) {
-                    e += k.ge[z] * re[o + z];
-                    g += k.gi[z] * ri[o + z];
-                }
-                const float v = (e - g) * k.scale;
-                qv[o] = (v < k.inhib) ? 0.f : v - k.inhib;
-                sum += (double)qv[o];
-            }
-            const int i = p / TC_T;
-            const unsigned e0 = ((unsigned)(tl.x0 + i) * Y + (tl.y0 + p - i * TC_T)) * TH + k0 + 4 * j;
-            co_put(Q, e0, qv, true, nbytes);
-        }
-    }
-    sum = co_wave_sum(sum);
-    if (lane == 0) s_red[wave] = sum;
-    co_lds_barrier();
-    if (tid == 0) {
-        double t = 0.0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) t += s_red[w];
-        st_wt(&part[blockIdx.x], t);
-    }
-    PC_STAMP(8, 4);
-}
-
-// Path integration (posecell_network.py:252-314) for one chunk: the per-layer shifted
-// 7 x 7 filter (:273 -> convolution.py:320-340) and clamp (:300) on the chunk's G + 6
-// layers, the theta filter (:310 -> :344-359) and clamp (:314) to its G layers, the
-// normalisation by the total (:343-345, applied once at the end), the argmax key
-// (:317-319) and one 16-byte write-through store per 4 layers of a cell.
-template <int G, int NW>
-__global__ __launch_bounds__(64 * NW) void pc_path_tc(const float* __restrict__ Q, int X, int Y, int TH, int gx,
-                                                      int nch, int nblk, float* __restrict__ P,
-                                                      const double* __restrict__ part, int npart,
-                                                      const float* __restrict__ filt, int nf, PcCtlTc ctl,
-                                                      unsigned long long* __restrict__ res_slot) {
-    using Gm = TcGeom<G>;
-    constexpr int NT = 64 * NW, NU = Gm::NU, LU = Gm::LU, NL = Gm::NL;
-    constexpr int PP = LU;                    // filter outputs [cell][L], 16-byte aligned rows
-    // the union image [u][v][local layer] (row pitch TC_UW cells), in dynamic LDS sized
-    // by the host for the step's widest chunk union (tc_union_lds_bytes): at small
-    // shifts more blocks share a CU
-    extern __shared__ __attribute__((aligned(16))) float s_w[];
-    __shared__ __attribute__((aligned(16))) float s_p[TC_T * TC_T * PP];
-    __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
-    __shared__ int s_dxy[NL], s_fo[NL];
-    __shared__ double s_tot;
-    __shared__ unsigned long long s_bk[NW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const TcTile tl = tc_tile(nblk, gx, nch);
-    const int k0 = tl.ch * G;
-    PC_STAMP(9, 0);
-    // wave 0: the normalisation partials' loads first (summed after the window's issue)
-    TcPartials pt;
-    if (wave == 0) pt.issue(part, npart);
-    // 1. the union of the chunk's layers' shifted 14 x 14 windows (host-formed)
-    const int uorg = ctl.uorg[tl.ch], uext = ctl.uext[tl.ch];
-    const int umx = (short)(uorg & 0xFFFF), umy = uorg >> 16, UW = uext & 0xFFFF, UH = uext >> 16;
-    // (ctl.urows: the union rows the launch's dynamic LDS holds, >= every fitting chunk's UW)
-    const bool uni = UW <= ctl.urows && UH <= TC_UW && UW <= X && UH <= Y;
-    if (uni) {
-        int gx0 = tl.x0 - HALF + umx, gy0 = tl.y0 - HALF + umy, u0 = (k0 >> 2) - 1;
-        gx0 = co_wrap(gx0, X);
-        gy0 = co_wrap(gy0, Y);
-        u0 += u0 < 0 ? (TH >> 2) : 0;
-        tc_window_dma<NU, TC_UW, TC_UW, NT>(Q, s_w, X, Y, TH, gx0, gy0, u0, UW, UH);
-    }
-    // the control of the chunk's layers (local L = global k0 - 3 + L), the filter table,
-    // and (wave 0) the normalisation total: in flight with the window
-    if (tid < NL) {
-        int g = k0 - HALF + tid;
-        g += g < 0 ? TH : 0;
-        g -= g >= TH ? TH : 0;
-        const int dx = co_centre(ctl.iox[g], X) - umx, dy = co_centre(ctl.ioy[g], Y) - umy;
-        s_dxy[tid] = uni ? (dx * TC_UW + dy) * LU : g;   // union: the window's offset; else the layer
-        s_fo[tid] = ctl.ifi[g] * ST_FTP;
-    }
-    for (int i = tid; i < nf * FT; i += NT) s_ftab[(i / FT) * ST_FTP + i % FT] = filt[i];
-    if (wave == 0) {
-        const double t = pt.sum(part, npart);
-        if (lane == 0) s_tot = t;
-    }
-    if (uni) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces have landed
-    co_lds_barrier();
-    PC_STAMP(9, 1);
-    // 2. 7 x 7 filter + clamp: task (layer L, column pair cg, row half hf) -> 4 x 2
-    //    outputs from 10 window rows of 8 cells; outputs into [cell][L]
-    constexpr int NCG = TC_T / 2, NTASK = NL * NCG * 2;
-    for (int t = tid; t < NTASK; t += NT) {
-        const int L = t % NL, rem = t / NL, hf = rem / NCG, cg = rem - hf * NCG;
-        float f[FT];
-        st_filter<float>(s_ftab + s_fo[L], f);
-        float acc[4][2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = 0.f;
-        if (uni) {
-            int wbase = s_dxy[L] + ((hf * 4) * TC_UW + 2 * cg) * LU + 1 + L;
-            asm volatile("" : "+v"(wbase));  // opaque: the reads keep immediate offsets
-            const float* win = s_w + wbase;
-#pragma unroll
-            for (int a = 0; a < 4 + 2 * HALF; ++a) {
-                float w[FL + 1];
-#pragma unroll
-                for (int q = 0; q < FL + 1; ++q) w[q] = win[(a * TC_UW + q) * LU];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int x = a - i;
-                    if (x < 0 || x >= FL) continue;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-#pragma unroll
-                        for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
-                }
-            }
-        } else {
-            // a union beyond the LDS image (layers' shifts spread by more than TC_MS
-            // cells, or a whole period): the layer's own window from memory
-            const int g = s_dxy[L];
-            const int bx = tl.x0 - HALF + co_centre(ctl.iox[g], X), by = tl.y0 - HALF + co_centre(ctl.ioy[g], Y);
-#pragma unroll
-            for (int a = 0; a < 4 + 2 * HALF; ++a) {
-                const int gr = rs::wrapi(bx + hf * 4 + a, X);
-                float w[FL + 1];
-#pragma unroll
-                for (int q = 0; q < FL + 1; ++q)
-                    w[q] = Q[((size_t)gr * Y + rs::wrapi(by + 2 * cg + q, Y)) * TH + g];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int x = a - i;
-                    if (x < 0 || x >= FL) continue;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-#pragma unroll
-                        for (int q = 0; q < FL; ++q) acc[i][c] += w[c + q] * f[x * FL + q];
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) s_p[((hf * 4 + i) * TC_T + 2 * cg + c) * PP + L] = pc_clamp(acc[i][c]);
-    }
-    co_lds_barrier();
-    PC_STAMP(9, 2);
-    // 3. theta filter + clamp + normalisation + argmax: task (cell p, group j of 4
-    //    output layers), output o = 4j + d (global k0 + o) takes L = o .. o + 6
-    const PcNorm<float> nrm(s_tot);
-    float zf[FL];
-#pragma unroll
-    for (int z = 0; z < FL; ++z) zf[z] = ctl.zf[z];
-    unsigned long long bk = 0ull;
-    {
-        constexpr int NG = G / 4;
-        const int nbytes = (int)min((size_t)X * Y * TH * sizeof(float), (size_t)INT_MAX);
-        for (int t = tid; t < TC_T * TC_T * NG; t += NT) {
-            const int p = t / NG, j = t - p * NG;
-            const co_f4* sv = reinterpret_cast<const co_f4*>(s_p + p * PP + 4 * j);
-            float r[12];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const co_f4 a = sv[q];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) r[4 * q + c] = a[c];
-            }
-            const int i = p / TC_T;
-            const unsigned e0 = ((unsigned)(tl.x0 + i) * Y + (tl.y0 + p - i * TC_T)) * TH + k0 + 4 * j;
-            co_f4 v;
-#pragma unroll
-            for (int o = 0; o < 4; ++o) {
-                float x = 0.f;
-#pragma unroll
-                for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
-                v[o] = nrm(pc_clamp(x));
-                bk = max(bk, argmax_key(v[o], e0 + o));
-            }
-            co_put(P, e0, v, true, nbytes);
-        }
-    }
-    bk = co_wave_max(bk);
-    if (lane == 0) s_bk[wave] = bk;
-    co_lds_barrier();
-    if (tid == 0) {
-#pragma unroll
-        for (int w = 1; w < NW; ++w) bk = max(bk, s_bk[w]);
-        atomicMax(res_slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
-    }
-    PC_STAMP(9, 3);
-}
-
 // Each step's RES_SLOTS packed argmax keys -> their max, stored straight into the
 // pinned host buffer (system-scope stores): one queued launch in place of a
 // device-to-host blit copy, which trailed the step by ~10 us (gap + copy kernel).
@@ -3244,9 +2830,6 @@ struct rs_pc {
                             // P and Q are then theta-fastest (C order (x, y, th))
     bool halo = false;      // one launch per step (RS_PC_FORM=halo): HF_T x HF_T tiles through all
                             // layers, the excitation recomputed on each tile's halo; P theta-fastest
-    bool tcExcCols = false;  // tc: the cols form's whole-extent excitation kernel (RS_PC_FORM=tc:G,NW,1)
-    int tcG = 0, tcNW = 4;  // theta-chunked column kernels (RS_PC_FORM=tc[:G[,NW[,E]]]; cols is set too:
-                            // theta-fastest P and Q, cgx x cgy tiles of TC_T, coNch = TH / G chunks)
     unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
     int cgx = 0, cgy = 0;   // column (or halo) tiles along x and y
     int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
@@ -3428,86 +3011,6 @@ inline StepOut step_out(const rs_pc* h, int s) {
     return step_out(h->dRes, h->dArgV, h->dArgI, h->esz, h->nPathBlocks, s);
 }
 
-// Control of step s for the theta-chunked path kernel: centred shifts per layer and, per
-// chunk, the union of the shifted 14 x 14 windows of its G + 6 layers (k0-3 .. k0+G+2).
-void make_ctl_tc(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
-                 const double* zf, PcCtlTc* c) {
-    const size_t b = (size_t)s * h->TH;
-    const int TH = h->TH, G = h->tcG;
-    for (int k = 0; k < TH; ++k) {
-        c->iox[k] = (short)co_centre(ox[b + k], h->X);
-        c->ioy[k] = (short)co_centre(oy[b + k], h->Y);
-        c->ifi[k] = (unsigned char)fidx[b + k];
-    }
-    for (int z = 0; z < FL; ++z) c->zf[z] = (float)zf[(size_t)s * FL + z];
-    for (int ch = 0; ch < h->coNch; ++ch) {
-        int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
-        for (int L = 0; L < G + 2 * HALF; ++L) {
-            const int g = rs::wrapi(ch * G - HALF + L, TH);
-            mnx = std::min(mnx, (int)c->iox[g]);
-            mxx = std::max(mxx, (int)c->iox[g]);
-            mny = std::min(mny, (int)c->ioy[g]);
-            mxy = std::max(mxy, (int)c->ioy[g]);
-        }
-        c->uorg[ch] = hf_pack((short)mnx, (short)mny);
-        c->uext[ch] = hf_pack((short)std::min(TC_W + mxx - mnx, 0x7FFF), (short)std::min(TC_W + mxy - mny, 0x7FFF));
-    }
-    // the LDS rows this step's launch needs: the widest chunk union that fits the image
-    // (a wider chunk reads its windows from memory); at least one row
-    int rows = 1;
-    for (int ch = 0; ch < h->coNch; ++ch) {
-        const int uw = c->uext[ch] & 0xFFFF, uh = c->uext[ch] >> 16;
-        if (uw <= TC_UW && uh <= TC_UW && uw <= h->X && uh <= h->Y) rows = std::max(rows, uw);
-    }
-    c->urows = rows;
-}
-
-// The instantiated (G, NW) pairs of the theta-chunked kernels.
-#define PC_TC_VARIANTS(X_) X_(12, 4) X_(24, 4) X_(24, 8) X_(36, 4) X_(36, 8)
-
-// One step of the theta-chunked form: the excitation, then (ctl != nullptr) the path kernel.
-int pc_launch_tc(rs_pc* h, const StepOut& so, const PcCtlTc* ctl, int prof_base) {
-    const dim3 g(h->cgx * h->cgy * h->coNch);
-    const float* P = static_cast<const float*>(h->dP);
-    float* Q = static_cast<float*>(h->dQ);
-    bool done = false;
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
-    if (h->tcExcCols) {   // the whole-extent column excitation, one block per 8 x 8 tile
-        const dim3 ge(h->cgx * h->cgy);
-        hipLaunchKernelGGL((pc_excite_cols<float, CO_TX, CO_TY, CO_NW, CO_DMA_TH, false, CO_DMA_TH>), ge,
-                           dim3(64 * CO_NW), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, h->cgy, (int)ge.x, Q,
-                           h->dPart, so.slot, h->TH, h->kf);
-        done = true;
-    }
-#define PC_TC_EXC(g_, nw_)                                                                                      \
-    if (!done && h->tcG == g_ && h->tcNW == nw_) {                                                            \
-        hipLaunchKernelGGL((pc_excite_tc<g_, nw_>), g, dim3(64 * nw_), 0, h->stream, P, h->X, h->Y, h->TH, h->cgx, \
-                           h->coNch, (int)g.x, Q, h->dPart, so.slot, h->kf);                                  \
-        done = true;                                                                                          \
-    }
-    PC_TC_VARIANTS(PC_TC_EXC)
-#undef PC_TC_EXC
-    RS_CHECK(done, RS_ERR_ARG, "no theta-chunked variant G=%d NW=%d", h->tcG, h->tcNW);
-    RS_HIP(hipGetLastError());
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 1], h->stream));
-    if (!ctl) return RS_OK;
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 2], h->stream));
-    done = false;
-#define PC_TC_PATH(g_, nw_)                                                                                   \
-    if (!done && h->tcG == g_ && h->tcNW == nw_) {                                                          \
-        hipLaunchKernelGGL((pc_path_tc<g_, nw_>), g, dim3(64 * nw_), tc_union_lds_bytes(g_, ctl->urows), h->stream, \
-                           Q, h->X, h->Y, h->TH, h->cgx,                                                    \
-                           h->coNch, (int)g.x, static_cast<float*>(h->dP), h->dPart, h->nPart,              \
-                           static_cast<const float*>(h->dFilt), h->nf, *ctl, so.slot);                      \
-        done = true;                                                                                        \
-    }
-    PC_TC_VARIANTS(PC_TC_PATH)
-#undef PC_TC_PATH
-    RS_HIP(hipGetLastError());
-    if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base + 3], h->stream));
-    return RS_OK;
-}
-
 // n steps of the halo form: one launch each (step s reads the state in one buffer,
 // scaled by the partials of the step before, and writes U into the other; the partial
 // sums ping-pong between the two halves of dPart), then pc_halo_finish: the state
@@ -3639,13 +3142,6 @@ int pc_launch_step(rs_pc* h, const StepOut& so, const CTL* ctl, int prof_base) {
     T* bmax = static_cast<T*>(so.bmax);
     unsigned* bidx = so.bidx;
     const T* filt = static_cast<const T*>(h->dFilt);
-    if (h->tcG > 0) {
-        // the theta-chunked form takes its own control (pc_run_direct); here only the
-        // excitation (rs_pc_excite)
-        RS_CHECK(ctl == nullptr, RS_ERR_STATE, "theta-chunked form: step control through pc_launch_tc");
-        if constexpr (std::is_same<T, float>::value) return pc_launch_tc(h, so, nullptr, prof_base);
-        RS_CHECK(false, RS_ERR_STATE, "theta-chunked form is float32 only");
-    }
     if (prof_base >= 0) RS_HIP(hipEventRecord(h->evPool[prof_base], h->stream));
     if (h->cols) {
         const dim3 g(h->cgx * h->cgy * h->coNch);
@@ -3759,7 +3255,7 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         return !e ? -1 : std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "ring") == 0 ? 0 : -1;
     }();
     const bool batch_inline = ctl_env >= 0 ? ctl_env == 1 : h->cols;
-    const bool inline_ctl = (n == 1 || batch_inline || h->tcG > 0) && h->TH <= CTL_INLINE_MAX;
+    const bool inline_ctl = (n == 1 || batch_inline) && h->TH <= CTL_INLINE_MAX;
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
@@ -3770,11 +3266,7 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
     if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
     for (int s = 0; s < n; ++s) {
         const int pb = pk ? 4 * s : -1;
-        if (h->tcG > 0) {
-            PcCtlTc c;
-            make_ctl_tc(h, s, ox, oy, fidx, zf, &c);
-            RS_TRY(pc_launch_tc(h, step_out(h, s), &c, pb));
-        } else if (inline_ctl) {
+        if (inline_ctl) {
             PcCtlInline c;
             make_ctl_inline(h, s, ox, oy, fidx, zf, &c);
             if (h->prec == RS_PREC_F32)
@@ -3991,43 +3483,6 @@ int pc_cols_set(rs_pc* h, int kc) {
     return RS_OK;
 }
 
-// The theta-chunked column form's limits: float32, whole tiles and whole 16-byte theta
-// units, chunks dividing the extent, windows that wrap with one conditional, the
-// control inline (16-bit shifts), the filter table in LDS, 32-bit buffer offsets.
-bool pc_tc_fit(const rs_pc* h, int G) {
-    return h->esz == 4 && G > 0 && G % 4 == 0 && h->TH % G == 0 && h->TH / G <= TC_NCH_MAX &&
-           h->TH <= CTL_INLINE_MAX && h->X % TC_T == 0 && h->Y % TC_T == 0 && h->X >= TC_UW && h->Y >= TC_UW &&
-           h->X <= 32767 && h->Y <= 32767 && h->nf <= RT_NFMAX && h->n * sizeof(float) <= (size_t)INT_MAX;
-}
-
-int pc_tc_set(rs_pc* h, int G, int nw) {
-    bool known = false;
-#define PC_TC_KNOWN(g_, nw_) known = known || (G == g_ && nw == nw_);
-    PC_TC_VARIANTS(PC_TC_KNOWN)
-#undef PC_TC_KNOWN
-    RS_CHECK(known, RS_ERR_ARG, "RS_PC_FORM=tc: no variant G=%d NW=%d", G, nw);
-    RS_CHECK(pc_tc_fit(h, G), RS_ERR_ARG,
-             "RS_PC_FORM=tc:%d needs float32, TH a multiple of %d (at most %d chunks), X and Y multiples of %d "
-             "and >= %d, at most %d path filters", G, G, TC_NCH_MAX, TC_T, TC_UW, RT_NFMAX);
-    // the path kernel's union image is dynamic LDS, up to TC_UW rows
-#define PC_TC_ATTR(g_, nw_)                                                                                  \
-    if (G == g_ && nw == nw_)                                                                                \
-        RS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&pc_path_tc<g_, nw_>),                     \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)tc_union_lds_bytes(g_, TC_UW)));
-    PC_TC_VARIANTS(PC_TC_ATTR)
-#undef PC_TC_ATTR
-    h->streamed = false;
-    h->cols = true;
-    h->halo = false;
-    h->tcG = G;
-    h->tcNW = nw;
-    h->cgx = h->X / TC_T;
-    h->cgy = h->Y / TC_T;
-    h->coKC = G;
-    h->coNch = h->TH / G;
-    return RS_OK;
-}
-
 // The halo form's limits: float32, the instantiated theta extent, the 16 x 16 layer
 // windows without self-overlap, the filter table in LDS, 32-bit buffer offsets.
 bool pc_halo_fit(const rs_pc* h) {
@@ -4064,15 +3519,6 @@ int pc_choose_form(rs_pc* h) {
                  HF_W, RT_NFMAX);
         return pc_halo_set(h);
     }
-    if (env && (std::strcmp(env, "tc") == 0 || std::strncmp(env, "tc:", 3) == 0)) {
-        int G = 24, nw = 4, ec = 0;
-        if (env[2] == ':') std::sscanf(env + 3, "%d,%d,%d", &G, &nw, &ec);
-        RS_TRY(pc_tc_set(h, G, nw));
-        RS_CHECK(!ec || (h->TH == CO_DMA_TH && CO_TX == TC_T && CO_TY == TC_T), RS_ERR_ARG,
-                 "RS_PC_FORM=tc:G,NW,1 (the cols excitation) needs TH == %d", CO_DMA_TH);
-        h->tcExcCols = ec != 0;
-        return RS_OK;
-    }
     if (env && std::strcmp(env, "rows") == 0) {
         RS_CHECK(h->tiling != 0, RS_ERR_ARG, "RS_PC_FORM=rows needs Y <= 128");
         h->streamed = false;
@@ -4097,8 +3543,7 @@ int pc_choose_form(rs_pc* h) {
         RS_CHECK(n >= 3, RS_ERR_ARG, "RS_PC_FORM=stream:BX,WR,WC[,KC], got '%s'", env);
     } else {
         RS_CHECK(env == nullptr || env[0] == 0 || std::strcmp(env, "stream") == 0, RS_ERR_ARG,
-                 "unknown RS_PC_FORM '%s' (rows | tiles | cols | tc[:G,NW] | halo | stream[:BX,WR,WC[,KC]])",
-                 env);
+                 "unknown RS_PC_FORM '%s' (rows | tiles | cols | halo | stream[:BX,WR,WC[,KC]])", env);
         // default: one pass per kernel (rows) while the whole grid fits in one wave of
         // blocks -- the step is latency-bound there (64x64x36: 17 us rows vs 23 us
         // streamed); streamed once the rows form's 4x theta-halo recompute dominates
@@ -4202,9 +3647,8 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         h->nPart = h->cgx * h->cgy;
         h->nPathBlocks = h->nPart;
     } else if (h->cols) {
-        h->nPathBlocks = h->cgx * h->cgy * h->coNch;
-        // (tc with the cols excitation: one excitation block per 8 x 8 tile, all layers)
-        h->nPart = h->tcExcCols ? h->cgx * h->cgy : h->nPathBlocks;
+        h->nPart = h->cgx * h->cgy * h->coNch;
+        h->nPathBlocks = h->nPart;
     } else if (h->streamed) {
         h->nPart = h->sg.gx * h->sg.gy * h->sg.gz;
         h->nPathBlocks = h->nPart;
@@ -4595,7 +4039,6 @@ const char* rs_pc_step_form(const rs_pc* h) {
     if (!h) return nullptr;
     if (h->streamed) return "stream";
     if (h->halo) return "halo";
-    if (h->tcG > 0) return "tc";
     if (h->cols) return "cols";
     return h->tiling ? "rows" : "tiles";
 }

@@ -117,11 +117,10 @@ int main(int argc, char** argv) {
     // wrote: a slot no block stamped (a phase this build does not stamp) is reported as
     // such, never as a difference against zero
     static const char* kname[NKID] = {"excite_rows", "path_rows", "excite_stream", "path_stream", "",
-                                      "excite_cols", "path_cols", "halo", "excite_tc", "path_tc"};
-    static const int kns[NKID] = {4, 6, 5, 5, 0, 5, 5, 7, 5, 4};
+                                      "excite_cols", "path_cols", "halo"};
+    static const int kns[NKID] = {4, 6, 5, 5, 0, 5, 5, 7};
     std::vector<int> kids;
     if (h->halo) kids = {7};
-    else if (h->tcG > 0) kids = {8, 9};
     else if (h->cols) kids = {5, 6};
     else if (h->streamed) kids = {2, 3};
     else if (h->tiling) kids = {0, 1};
@@ -231,37 +230,6 @@ int main(int argc, char** argv) {
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
         printf("halo step alone: %.2f us/launch\n", 1e3 * t / reps);
-        rs_pc_destroy(h);
-        return 0;
-    }
-    if (h->tcG > 0) {  // back-to-back launch costs of the theta-chunked kernels
-        hipEvent_t c0, c1;
-        CK(hipEventCreate(&c0));
-        CK(hipEventCreate(&c1));
-        const dim3 g(h->cgx * h->cgy * h->coNch), b(64 * h->tcNW);
-        const int reps = 500;
-        float t = 0;
-        CK(hipEventRecord(c0, h->stream));
-        for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(empty_kernel, g, b, 0, h->stream, nullptr);
-        CK(hipEventRecord(c1, h->stream));
-        CK(hipEventSynchronize(c1));
-        CK(hipEventElapsedTime(&t, c0, c1));
-        printf("empty kernel, same grid: %.2f us/launch\n", 1e3 * t / reps);
-        PcCtlTc c;
-        make_ctl_tc(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
-        const StepOut so = step_out(h, 0);
-        CK(hipEventRecord(c0, h->stream));
-        for (int i = 0; i < reps; ++i) pc_launch_tc(h, so, nullptr, -1);
-        CK(hipEventRecord(c1, h->stream));
-        CK(hipEventSynchronize(c1));
-        CK(hipEventElapsedTime(&t, c0, c1));
-        printf("excite alone: %.2f us/launch\n", 1e3 * t / reps);
-        CK(hipEventRecord(c0, h->stream));
-        for (int i = 0; i < reps; ++i) pc_launch_tc(h, so, &c, -1);
-        CK(hipEventRecord(c1, h->stream));
-        CK(hipEventSynchronize(c1));
-        CK(hipEventElapsedTime(&t, c0, c1));
-        printf("excite + path: %.2f us/step\n", 1e3 * t / reps);
         rs_pc_destroy(h);
         return 0;
     }

@@ -142,8 +142,6 @@ def traffic_of(configs, tag):
             traffic['pose_cell'][form] = rec
         elif c in PCS:
             form, shape = PCS[c]
-            if any(k.startswith('pc_excite_tc') for k in ks):
-                form = 'tc'    # the theta-chunked column form (the default at 128x128x72 from round 5)
             ex = [k for k in ks if k.startswith('pc_excite') and ks[k].get('trace')]
             pa = [k for k in ks if k.startswith('pc_path') and ks[k].get('trace')]
             if not (ex and pa):
@@ -207,7 +205,7 @@ def main():
     if f:
         shutil.copy(f, os.path.join(raw, 'bench_kernel_stats.csv'))
     for c, rec in list(traffic['scans'].items()) + list(traffic['pose_cell'].items()):
-        cfg = c if c in SCANS else {'rows': 'pc64', 'halo': 'pc64', 'cols': 'pc128', 'tc': 'pc128'}[c]
+        cfg = c if c in SCANS else {'rows': 'pc64', 'halo': 'pc64', 'cols': 'pc128'}[c]
         rec['kernel_us_source'] = (f'profiles/{a.tag}/{cfg}_kernel_trace.csv (median over the dispatches; '
                                    f'the --stats average is kernel_us_rocprof_avg, {cfg}_kernel_stats.csv)')
         rec['counter_source'] = f'profiles/{a.tag}/{cfg}_counters.csv'
