@@ -191,10 +191,19 @@ const char* rs_pc_step_form(const rs_pc* h);
  *                          write shows up as NaN state or a wrong peak;
  *   RS_PC_DBG_SKIP_EXPORT  the next update/run leaves the host result words
  *                          unwritten: the call must fail with RS_ERR_HIP (the
- *                          check that every step's argmax reached the host). */
+ *                          check that every step's argmax reached the host);
+ *   RS_PC_DBG_HALO_SETTLE  (halo form) every later call ends with the state
+ *                          normalised by the finishing pass instead of left
+ *                          unnormalised for the next call (A/B of the two paths);
+ *   RS_PC_DBG_HALO_AMBIG   (rs_pc_debug_value) how many calls had their last step
+ *                          keyed by the finishing pass because a cell lay within a
+ *                          relative 2^-20 of the peak (pc_halo_export's RES_AMBIG). */
 #define RS_PC_DBG_POISON      1
 #define RS_PC_DBG_SKIP_EXPORT 2
+#define RS_PC_DBG_HALO_SETTLE 3
+#define RS_PC_DBG_HALO_AMBIG  4
 int rs_pc_debug(rs_pc* h, int op);
+int rs_pc_debug_value(rs_pc* h, int op, int64_t* value);
 
 /* ------------------------------------------------------------------------ */
 /* View templates                                                            */

@@ -26,6 +26,8 @@ RS_PREC_F32 = 0
 RS_PREC_F64 = 1
 RS_PC_DBG_POISON = 1
 RS_PC_DBG_SKIP_EXPORT = 2
+RS_PC_DBG_HALO_SETTLE = 3
+RS_PC_DBG_HALO_AMBIG = 4
 RS_VT_FROZEN = 0
 RS_VT_SEQUENTIAL = 1
 RS_UNIQUE_ID_BYTES = 128
@@ -93,6 +95,7 @@ SIGNATURES = {
     'rs_pc_kernel_ms': (ctypes.c_int, [_vp, _f64p]),
     'rs_pc_step_form': (ctypes.c_char_p, [_vp]),
     'rs_pc_debug': (ctypes.c_int, [_vp, ctypes.c_int]),
+    'rs_pc_debug_value': (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]),
     'rs_vt_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                     ctypes.c_int64, ctypes.c_int, ctypes.POINTER(_vp)]),
     'rs_vt_destroy': (ctypes.c_int, [_vp]),

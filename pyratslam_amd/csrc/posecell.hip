@@ -2025,6 +2025,11 @@ constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;
 constexpr int HF_YJ = HF_W * HF_Q + 10;       // y-pass outputs per layer (pitch: the x pass reads conflict-free)
 constexpr int HF_QJ = HF_Q * HF_Q + 4;        // Q window per layer
 constexpr int HF_EXP_MAX = 64;                // steps whose keys pc_halo_finish exports itself
+constexpr float HF_NEAR = 0x1p-20f;           // relative margin of a possible rounding tie (pc_halo_export)
+// A step's result word when its last-step records cannot settle the first maximum of the
+// scaled state (a cell within HF_NEAR of the maximum): never a valid key (a key's low
+// word is ~lin >= 2, lin < X*Y*TH < 2^32 - 1, rs_pc_create)
+constexpr unsigned long long RES_AMBIG = 1ull;
 
 // One step's control, a kernel argument (formed on the host by make_ctl_halo).
 struct PcCtlHalo {
@@ -2068,7 +2073,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     const float* __restrict__ U, int X, int Y, int gx, int nblk, int ulo, int uext, float* __restrict__ Uo,
     const double* __restrict__ part_in, int npart_in, double* __restrict__ part_out,
     unsigned long long* __restrict__ slot_prev, unsigned long long* __restrict__ slot_zero,
-    const float* __restrict__ filt, int nf, PcCtlHalo ctl, SepKernel<float> k) {
+    const float* __restrict__ filt, int nf, PcCtlHalo ctl, SepKernel<float> k,
+    unsigned long long* __restrict__ rec) {
     constexpr int TH = HF_TH, NV = TH / 4;   // 16-byte pieces per theta column
     static_assert(TH % 4 == 0, "theta columns of whole 16-byte pieces");
     constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
@@ -2083,7 +2089,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_fo[TH];
     __shared__ double s_red[HF_NW];
-    __shared__ unsigned long long s_bk[HF_NW];
+    __shared__ unsigned long long s_bk[HF_NW], s_rk[HF_NW];
+    __shared__ int s_cnt[HF_NW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tile = st_tile(blockIdx.x, nblk);
@@ -2418,6 +2425,13 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     }
     float* s_po = s_b;
+    // rec (the last step of a call that leaves the state unnormalised, pc_run_halo):
+    // the key of the block's largest output U and, below, how many of its outputs lie
+    // within a relative 2^-20 of it (HF_NEAR): P = U * (1/t) rounds monotonically, so the
+    // first maximum of P is the first maximum of U unless another cell lies that close
+    unsigned long long rk = 0ull;
+    co_f4 uv = {0.f, 0.f, 0.f, 0.f};
+    bool has_uv = false;
     if constexpr (!EXC) {
         co_lds_barrier();
         PC_STAMP(7, 4);
@@ -2484,6 +2498,12 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
             const unsigned lin = ((unsigned)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g;
             co_put(Uo, lin, v, wt, nbytes);
+            if (rec) {
+#pragma unroll
+                for (int o = 0; o < 4; ++o) rk = max(rk, argmax_key(v[o], lin + o));
+                uv = v;
+                has_uv = true;
+            }
             }
         }
     }
@@ -2494,7 +2514,31 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         bk = co_wave_max(bk);
         if (lane == 0) s_bk[wave] = bk;
     }
+    if (rec) {
+        rk = co_wave_max(rk);
+        if (lane == 0) s_rk[wave] = rk;
+    }
     co_lds_barrier();
+    if (rec) {
+        // the block's record: its largest U's key and the count of its outputs within
+        // HF_NEAR of that value (the maximum itself included)
+        unsigned long long m = s_rk[0];
+#pragma unroll
+        for (int w = 1; w < HF_NW; ++w) m = max(m, s_rk[w]);
+        const float mv = __uint_as_float((unsigned)(m >> 32)), thr = mv - mv * HF_NEAR;
+        int c = 0;
+#pragma unroll
+        for (int o = 0; o < 4; ++o) c += __popcll(__ballot(has_uv && uv[o] >= thr));
+        if (lane == 0) s_cnt[wave] = c;
+        co_lds_barrier();
+        if (tid == 0) {
+            int cnt = 0;
+#pragma unroll
+            for (int w = 0; w < HF_NW; ++w) cnt += s_cnt[w];
+            st_wt(&rec[2 * blockIdx.x], m);
+            st_wt(&rec[2 * blockIdx.x + 1], (unsigned long long)cnt);
+        }
+    }
     if (tid == 0) {
         double bsum = 0.0;
 #pragma unroll
@@ -2596,6 +2640,42 @@ __global__ __launch_bounds__(64) void pc_res_export(const unsigned long long* __
         for (int k = 1; k < RES_SLOTS / 64; ++k) m = max(m, r[threadIdx.x + 64 * k]);
         m = co_wave_max(m);
         if (threadIdx.x == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The halo form's key export for a call that leaves its state unnormalised: steps
+// 0 .. n-2 as pc_res_export (each keyed by the next launch from the scaled state it
+// loaded); step n-1 from the last launch's per-block records of U.  P = U * (1/t) with
+// t > 0 (or P = U when t == 0, or U / t where 1/t is not finite) rounds monotonically,
+// so P's first maximum is U's, unless some other cell's U lies within HF_NEAR of the
+// maximum (it might round to the same P, and the earlier index would win): then the
+// word is RES_AMBIG and the host settles the state exactly (pc_halo_finish).  NaN, 0
+// and inf maxima are exact (their products are the same value for every such cell).
+__global__ __launch_bounds__(64) void pc_halo_export(const unsigned long long* __restrict__ res, int n,
+                                                     const unsigned long long* __restrict__ rec, int nrec,
+                                                     unsigned long long* host) {
+    const int lane = threadIdx.x;
+    for (int s = blockIdx.x; s < n; s += gridDim.x) {
+        unsigned long long m = 0ull;
+        if (s < n - 1 || rec == nullptr) {
+            const unsigned long long* r = res + (size_t)s * RES_SLOTS;
+#pragma unroll
+            for (int k = 0; k < RES_SLOTS / 64; ++k) m = max(m, r[lane + 64 * k]);
+            m = co_wave_max(m);
+        } else {
+            for (int b = lane; b < nrec; b += 64) m = max(m, rec[2 * b]);
+            m = co_wave_max(m);
+            const float gv = __uint_as_float((unsigned)(m >> 32)), thr = gv - gv * HF_NEAR;
+            const bool exact = !(gv > 0.f) || gv == __builtin_inff() || gv != gv;   // 0 (all zero), inf, NaN
+            bool amb = false;
+            for (int b = lane; b < nrec; b += 64) {
+                const unsigned long long kb = rec[2 * b];
+                amb |= kb == m ? rec[2 * b + 1] > 1ull : __uint_as_float((unsigned)(kb >> 32)) >= thr;
+            }
+            amb = __ballot(amb) != 0ull;
+            if (!exact && amb) m = RES_AMBIG;
+        }
+        if (lane == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2831,6 +2911,11 @@ struct rs_pc {
     bool halo = false;      // one launch per step (RS_PC_FORM=halo): HF_T x HF_T tiles through all
                             // layers, the excitation recomputed on each tile's halo; P theta-fastest
     unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
+    unsigned long long* dRec = nullptr;  // halo: the last launch's per-block (key of max U, near count)
+    bool haloPend = false;  // halo: the state is U, unnormalised, in buffer haloCur (0 dP, 1 dQ) with
+    int haloCur = 0, haloPart = 0;  // its partial sums in half haloPart of dPart (pc_halo_settle)
+    long haloAmbig = 0;     // calls whose last step was keyed by the finishing pass (RES_AMBIG)
+    bool haloSettleAlways = false;  // rs_pc_debug(RS_PC_DBG_HALO_SETTLE)
     int cgx = 0, cgy = 0;   // column (or halo) tiles along x and y
     int coKC = 0, coNch = 1;  // layers per theta chunk (KC == TH: whole extent, no halo), chunks
     int sbx = 1, swr = 8, swc = 1;  // streaming tile: BX rows per wave, WR row groups, WC column tiles
@@ -3011,67 +3096,124 @@ inline StepOut step_out(const rs_pc* h, int s) {
     return step_out(h->dRes, h->dArgV, h->dArgI, h->esz, h->nPathBlocks, s);
 }
 
+// The halo form's state left unnormalised by a call (U in buffer haloCur, its partial
+// sums in half haloPart of dPart), normalised into dP: the entry points that read or
+// change the state directly (read, write, inject, get_max, total, excite, debug) settle
+// it first.  (The next call's first launch consumes it as it is: it scales on load.)
+int pc_halo_settle(rs_pc* h) {
+    if (!h->haloPend) return RS_OK;
+    float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
+    const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
+    hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
+                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
+                       nullptr, nullptr, (int)(h->n * sizeof(float)), 0);
+    RS_HIP(hipGetLastError());
+    h->haloPend = false;
+    h->haloCur = 0;
+    return RS_OK;
+}
+
 // n steps of the halo form: one launch each (step s reads the state in one buffer,
 // scaled by the partials of the step before, and writes U into the other; the partial
-// sums ping-pong between the two halves of dPart), then pc_halo_finish: the state
-// normalised back into dP, the last step keyed, every step's key exported to the host
-// (its last block, by a counter), the float64 volume for an eager readback; one host
-// sync.  (An update() that ended in its own launch -- its last block keying the new
-// state from per-block records, the state left unnormalised until the next load --
-// measured slower than this second launch: 27.5 vs 26.3 us per call at 64x64x36, the
-// records' drain, the counter atomic and the records' loads being memory round trips in
-// series; with the records stored straight into host memory the host's wait grew to
-// 28.9 us for a 13.4 us call.)
+// sums ping-pong between the two halves of dPart).  Then, by default, the call ends with
+// the state left unnormalised (haloPend) and one small export launch (pc_halo_export):
+// steps 0 .. n-2 keyed by the launch after each, step n-1 from the last launch's
+// per-block records of U -- the finishing pass over the volume (pc_halo_finish) is off
+// the per-call path (update() at 64x64x36: about 4 us of device time per call).  With an
+// eager readback (the float64 volume into the caller's pinned array), or when the
+// records cannot settle the last step's first maximum (RES_AMBIG: a cell within
+// HF_NEAR of the peak), pc_halo_finish normalises the state into dP, keys it and
+// exports.  One host sync (two for RES_AMBIG).  RS_PC_HALO_SETTLE=1 always finishes.
 int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                 const double* zf, int32_t* out_xyz) {
     RS_TRY(pc_grow_steps(h, n));
     const bool pk = h->profiling && h->profKernels;
     if (pk) RS_TRY(pc_ensure_events(h, (size_t)2 * n + 2));
     for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
-    if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
-    float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
-    const dim3 grid(h->cgx * h->cgy);
-    for (int s = 0; s < n; ++s) {
-        PcCtlHalo c;
-        make_ctl_halo(h, s, ox, oy, fidx, zf, &c);
-        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
-        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[s & 1], h->X, h->Y,
-                           h->cgx, (int)grid.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), buf[(s + 1) & 1],
-                           h->dPart + (size_t)((s + 1) & 1) * h->nPart, s == 0 ? 0 : h->nPart,
-                           h->dPart + (size_t)(s & 1) * h->nPart,
-                           s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
-                           h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->kf);
-        RS_HIP(hipGetLastError());
-        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
-    }
-    // RS_PC_HALO_EXPORT=kernel: the keys exported by a pc_res_export launch instead of
-    // the finishing kernel's last block (A/B); RS_PC_HALO_FENCE=1: the hand-off fenced
-    static const bool export_kernel = [] {
+    // RS_PC_HALO_SETTLE=1: every call ends normalised (the round-4 sequence, A/B);
+    // RS_PC_HALO_EXPORT=last: that finishing kernel's last block exports the keys;
+    // RS_PC_HALO_FENCE=1: that hand-off fenced
+    static const bool settle_env = [] {
+        const char* e = std::getenv("RS_PC_HALO_SETTLE");
+        return e && std::strcmp(e, "1") == 0;
+    }();
+    static const bool export_last = [] {
         const char* e = std::getenv("RS_PC_HALO_EXPORT");
-        return e && std::strcmp(e, "kernel") == 0;
+        return e && std::strcmp(e, "last") == 0;
     }();
     static const int fence = [] {
         const char* e = std::getenv("RS_PC_HALO_FENCE");
         return e && std::strcmp(e, "1") == 0 ? 1 : 0;
     }();
-    const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX && !export_kernel;
-    const int n4 = (int)(h->n / 4);
-    const int nb = std::min(1024, (n4 + 255) / 256);
-    if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
-    hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[n & 1], buf[0], n4,
-                       h->dPart + (size_t)((n - 1) & 1) * h->nPart, h->nPart,
-                       h->dRes + (size_t)(n - 1) * RES_SLOTS, h->dRes, own_export ? n : 0, h->dCounter,
-                       h->hResDev, h->exportDev, (int)(h->n * sizeof(float)), fence);
-    RS_HIP(hipGetLastError());
-    if (!h->dbgSkipExport && !own_export) {
-        hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
-                           h->hResDev);
+    const bool lazy = h->exportDev == nullptr && !settle_env && !h->haloSettleAlways;
+    if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
+    float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
+    const dim3 grid(h->cgx * h->cgy);
+    const bool pend = h->haloPend;
+    const int c0 = pend ? h->haloCur : 0;          // the buffer step 0 reads
+    const int p0 = pend ? (h->haloPart ^ 1) : 0;   // the partials half step 0 writes
+    for (int s = 0; s < n; ++s) {
+        PcCtlHalo c;
+        make_ctl_halo(h, s, ox, oy, fidx, zf, &c);
+        const double* part_in = s > 0 ? h->dPart + (size_t)((p0 + s - 1) & 1) * h->nPart
+                                      : h->dPart + (size_t)(pend ? h->haloPart : 0) * h->nPart;
+        const int npart_in = s > 0 || pend ? h->nPart : 0;
+        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
+        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[(c0 + s) & 1], h->X, h->Y,
+                           h->cgx, (int)grid.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), buf[(c0 + s + 1) & 1],
+                           part_in, npart_in, h->dPart + (size_t)((p0 + s) & 1) * h->nPart,
+                           s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
+                           h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
+                           lazy && s == n - 1 ? h->dRec : nullptr);
         RS_HIP(hipGetLastError());
+        if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
     }
+    const int cl = (c0 + n) & 1, pl = (p0 + n - 1) & 1;   // where the last U and its partials are
+    const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
+    auto finish = [&](int nexp_own, double* xp) -> int {
+        hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[cl], buf[0], n4,
+                           h->dPart + (size_t)pl * h->nPart, h->nPart, h->dRes + (size_t)(n - 1) * RES_SLOTS,
+                           h->dRes, nexp_own, h->dCounter, h->hResDev, xp, (int)(h->n * sizeof(float)), fence);
+        RS_HIP(hipGetLastError());
+        h->haloPend = false;
+        h->haloCur = 0;
+        return RS_OK;
+    };
+    if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
+    if (lazy) {
+        if (!h->dbgSkipExport) {
+            hipLaunchKernelGGL(pc_halo_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
+                               h->dRec, (int)grid.x, h->hResDev);
+            RS_HIP(hipGetLastError());
+        }
+        h->haloPend = true;
+        h->haloCur = cl;
+        h->haloPart = pl;
+    } else {
+        const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX && export_last;
+        RS_TRY(finish(own_export ? n : 0, h->exportDev));
+        if (!h->dbgSkipExport && !own_export) {
+            hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
+                               h->hResDev);
+            RS_HIP(hipGetLastError());
+        }
+    }
+    const bool skipped = h->dbgSkipExport;
     h->dbgSkipExport = false;
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n + 1], h->stream));
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    if (lazy && !skipped && h->hRes[n - 1] == RES_AMBIG) {
+        // a cell within HF_NEAR of the last step's peak: key the normalised state itself
+        // (its slots were zeroed by the last launch and nothing has reduced into them)
+        h->hRes[n - 1] = RES_NONE;
+        RS_TRY(finish(0, nullptr));
+        hipLaunchKernelGGL(pc_res_export, dim3(1), dim3(64), 0, h->stream, h->dRes + (size_t)(n - 1) * RES_SLOTS, 1,
+                           h->hResDev + (n - 1));
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipStreamSynchronize(h->stream));
+        ++h->haloAmbig;
+    }
     for (int s = 0; s < n; ++s)
         RS_CHECK(h->hRes[s] != RES_NONE, RS_ERR_HIP,
                  "step %d of %d: its argmax key did not reach the host result buffer after the "
@@ -3683,6 +3825,7 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     // (the halo form keeps two steps' partial sums: the one it reads, the one it writes)
     PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart * 2));
     PC_ALLOC(hipMemsetAsync(h->dPart, 0, sizeof(double) * h->nPart * 2, h->stream));
+    PC_ALLOC(hipMalloc(&h->dRec, sizeof(unsigned long long) * 2 * h->nPart));
     PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
     PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
@@ -3717,7 +3860,8 @@ int rs_pc_destroy(rs_pc* h) {
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->hRead) (void)hipHostFree(h->hRead);
-    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, (void*)h->dCounter, h->dBmax, (void*)h->dBidx, h->dArgV,
+    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, (void*)h->dCounter, (void*)h->dRec, h->dBmax,
+                    (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
         if (p) (void)hipFree(p);
@@ -3755,6 +3899,7 @@ int rs_pc_excite(rs_pc* h) {
     rs::clear_error();
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     if (h->halo) {
         // the halo kernel's excitation-only instance: no shifts, Q of the own cells
         PcCtlHalo c{};
@@ -3763,7 +3908,8 @@ int rs_pc_excite(rs_pc* h) {
         hipLaunchKernelGGL((pc_step_halo<true>), dim3(h->cgx * h->cgy), dim3(HF_NT), 0, h->stream,
                            static_cast<const float*>(h->dP), h->X, h->Y, h->cgx, h->cgx * h->cgy,
                            hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), static_cast<float*>(h->dQ), h->dPart, 0,
-                           h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf);
+                           h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
+                           nullptr);
         RS_HIP(hipGetLastError());
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
                            static_cast<float*>(h->dQ), h->n, h->dPart, h->nPart);
@@ -3911,6 +4057,7 @@ int rs_pc_inject(rs_pc* h, double energy, int x, int y, int th) {
     RS_CHECK(x >= 0 && x < h->X && y >= 0 && y < h->Y && th >= 0 && th < h->TH, RS_ERR_ARG,
              "inject location (%d, %d, %d) outside grid (%d, %d, %d)", x, y, th, h->X, h->Y, h->TH);
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     // the column form keeps P theta-fastest (C order); the others layer-major
     const size_t idx = pc_thfast(h) ? ((size_t)x * h->Y + y) * h->TH + th : ((size_t)th * h->X + x) * h->Y + y;
     if (h->prec == RS_PREC_F32)
@@ -3929,6 +4076,7 @@ int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]) {
     rs::clear_error();
     RS_CHECK(h && out_xyz, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     if (h->prec == RS_PREC_F32) return pc_argmax_impl<float>(h, out_xyz);
     return pc_argmax_impl<double>(h, out_xyz);
 }
@@ -3937,6 +4085,7 @@ int rs_pc_read(rs_pc* h, double* host) {
     rs::clear_error();
     RS_CHECK(h && host, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     // The export kernel writes the float64 C-order volume straight into pinned host
     // memory (one launch, no copy engine), then the host copies it into the caller's
     // array; RS_PC_READ=dma exports to HBM and copies with hipMemcpyAsync instead.
@@ -3968,6 +4117,7 @@ int rs_pc_read_pinned(rs_pc* h, double* pinned) {
     RS_CHECK(h && pinned, RS_ERR_ARG, "null argument");
     RS_CHECK(reinterpret_cast<uintptr_t>(pinned) % 16 == 0, RS_ERR_ARG, "pinned buffer not 16-byte aligned");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     double* dst = nullptr;
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), pinned, 0));
     const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
@@ -3986,6 +4136,8 @@ int rs_pc_write(rs_pc* h, const double* host) {
     rs::clear_error();
     RS_CHECK(h && host, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
+    h->haloPend = false;  // (halo: the whole state is replaced)
+    h->haloCur = 0;
     RS_HIP(hipMemcpyAsync(h->dTmp, host, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_import_kernel<float>), dim3(256), dim3(NT), 0, h->stream, h->dTmp,
@@ -4002,6 +4154,7 @@ int rs_pc_total(rs_pc* h, double* total) {
     rs::clear_error();
     RS_CHECK(h && total, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_total_kernel<float>), dim3(1), dim3(NT), 0, h->stream,
                            static_cast<const float*>(h->dP), h->n, h->dScalar);
@@ -4047,6 +4200,7 @@ int rs_pc_debug(rs_pc* h, int op) {
     rs::clear_error();
     RS_CHECK(h, RS_ERR_STATE, "null pose-cell handle");
     RS_HIP(hipSetDevice(h->device));
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     if (op == RS_PC_DBG_POISON) {
         // every buffer a step writes before it reads: all bits set (NaN volumes, the
         // largest possible argmax key in every slot of every step)
@@ -4066,7 +4220,20 @@ int rs_pc_debug(rs_pc* h, int op) {
         h->dbgSkipExport = true;
         return RS_OK;
     }
+    if (op == RS_PC_DBG_HALO_SETTLE) {
+        h->haloSettleAlways = true;
+        return RS_OK;
+    }
+
     RS_CHECK(false, RS_ERR_ARG, "unknown rs_pc_debug op %d", op);
+}
+
+int rs_pc_debug_value(rs_pc* h, int op, int64_t* value) {
+    rs::clear_error();
+    RS_CHECK(h && value, RS_ERR_ARG, "null argument");
+    RS_CHECK(op == RS_PC_DBG_HALO_AMBIG, RS_ERR_ARG, "unknown rs_pc_debug_value op %d", op);
+    *value = h->haloAmbig;
+    return RS_OK;
 }
 
 }  // extern "C"

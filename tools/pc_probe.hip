@@ -225,7 +225,7 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, X, Y, h->cgx,
                                (int)g.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), (float*)h->dQ,
                                h->dPart, h->nPart, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
-                               (const float*)h->dFilt, h->nf, c, h->kf);
+                               (const float*)h->dFilt, h->nf, c, h->kf, nullptr);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
         CK(hipEventElapsedTime(&t, c0, c1));
