@@ -2535,8 +2535,10 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             int cnt = 0;
 #pragma unroll
             for (int w = 0; w < HF_NW; ++w) cnt += s_cnt[w];
-            st_wt(&rec[2 * blockIdx.x], m);
-            st_wt(&rec[2 * blockIdx.x + 1], (unsigned long long)cnt);
+            // one 16-byte store: the record may live in pinned host memory (a one-step
+            // call, pc_run_halo), where each store is a PCIe write
+            typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u2*>(rec + 2 * blockIdx.x) = u2{m, (unsigned long long)cnt};
         }
     }
     if (tid == 0) {
@@ -2912,6 +2914,8 @@ struct rs_pc {
                             // layers, the excitation recomputed on each tile's halo; P theta-fastest
     unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
     unsigned long long* dRec = nullptr;  // halo: the last launch's per-block (key of max U, near count)
+    unsigned long long* hRec = nullptr;  // ... for a one-step call: pinned host records (hRecDev on the device)
+    unsigned long long* hRecDev = nullptr;
     bool haloPend = false;  // halo: the state is U, unnormalised, in buffer haloCur (0 dP, 1 dQ) with
     int haloCur = 0, haloPart = 0;  // its partial sums in half haloPart of dPart (pc_halo_settle)
     long haloAmbig = 0;     // calls whose last step was keyed by the finishing pass (RES_AMBIG)
@@ -3096,6 +3100,30 @@ inline StepOut step_out(const rs_pc* h, int s) {
     return step_out(h->dRes, h->dArgV, h->dArgI, h->esz, h->nPathBlocks, s);
 }
 
+// pc_halo_export's last-step rule on the host, over records in pinned host memory: the
+// largest key, or RES_AMBIG when another cell may round to the same scaled value; RES_NONE
+// when a block's record is missing (a record's key is never 0).
+unsigned long long halo_key_from_records(const unsigned long long* rec, int nrec) {
+    unsigned long long m = 0ull;
+    for (int b = 0; b < nrec; ++b) {
+        if (rec[2 * b] == 0ull) return RES_NONE;
+        m = std::max(m, rec[2 * b]);
+    }
+    auto val = [](unsigned long long k) {
+        const unsigned u = (unsigned)(k >> 32);
+        float f;
+        std::memcpy(&f, &u, sizeof(f));
+        return f;
+    };
+    const float gv = val(m), thr = gv - gv * HF_NEAR;
+    if (!(gv > 0.f) || std::isinf(gv) || std::isnan(gv)) return m;   // 0, inf, NaN maxima are exact
+    for (int b = 0; b < nrec; ++b) {
+        const unsigned long long kb = rec[2 * b];
+        if (kb == m ? rec[2 * b + 1] > 1ull : val(kb) >= thr) return RES_AMBIG;
+    }
+    return m;
+}
+
 // The halo form's state left unnormalised by a call (U in buffer haloCur, its partial
 // sums in half haloPart of dPart), normalised into dP: the entry points that read or
 // change the state directly (read, write, inject, get_max, total, excite, debug) settle
@@ -3145,7 +3173,16 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         const char* e = std::getenv("RS_PC_HALO_FENCE");
         return e && std::strcmp(e, "1") == 0 ? 1 : 0;
     }();
+    static const bool rec_device = [] {
+        const char* e = std::getenv("RS_PC_HALO_REC");
+        return e && std::strcmp(e, "device") == 0;
+    }();
     const bool lazy = h->exportDev == nullptr && !settle_env && !h->haloSettleAlways;
+    // a one-step call: the blocks' records go straight to pinned host memory and the host
+    // reduces them after its sync (no export launch; RS_PC_HALO_REC=device: the export
+    // kernel, as for batches)
+    const bool host_rec = lazy && n == 1 && h->hRec && !rec_device;
+    if (host_rec) std::memset(h->hRec, 0, sizeof(unsigned long long) * 2 * h->nPart);
     if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
     float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
     const dim3 grid(h->cgx * h->cgy);
@@ -3164,7 +3201,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                            part_in, npart_in, h->dPart + (size_t)((p0 + s) & 1) * h->nPart,
                            s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
                            h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
-                           lazy && s == n - 1 ? h->dRec : nullptr);
+                           lazy && s == n - 1 ? (host_rec ? h->hRecDev : h->dRec) : nullptr);
         RS_HIP(hipGetLastError());
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s + 1], h->stream));
     }
@@ -3181,7 +3218,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     };
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
     if (lazy) {
-        if (!h->dbgSkipExport) {
+        if (!h->dbgSkipExport && !host_rec) {
             hipLaunchKernelGGL(pc_halo_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
                                h->dRec, (int)grid.x, h->hResDev);
             RS_HIP(hipGetLastError());
@@ -3203,6 +3240,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n + 1], h->stream));
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
     RS_HIP(hipStreamSynchronize(h->stream));
+    if (host_rec && !skipped) h->hRes[n - 1] = halo_key_from_records(h->hRec, (int)grid.x);
     if (lazy && !skipped && h->hRes[n - 1] == RES_AMBIG) {
         // a cell within HF_NEAR of the last step's peak: key the normalised state itself
         // (its slots were zeroed by the last launch and nothing has reduced into them)
@@ -3826,6 +3864,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     PC_ALLOC(hipMalloc(&h->dPart, sizeof(double) * h->nPart * 2));
     PC_ALLOC(hipMemsetAsync(h->dPart, 0, sizeof(double) * h->nPart * 2, h->stream));
     PC_ALLOC(hipMalloc(&h->dRec, sizeof(unsigned long long) * 2 * h->nPart));
+    if (h->halo) {
+        PC_ALLOC(hipHostMalloc(&h->hRec, sizeof(unsigned long long) * 2 * h->nPart,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+        PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hRecDev), h->hRec, 0));
+    }
     PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
     PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
@@ -3866,6 +3909,7 @@ int rs_pc_destroy(rs_pc* h) {
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
         if (p) (void)hipFree(p);
     if (h->hRes) (void)hipHostFree(h->hRes);
+    if (h->hRec) (void)hipHostFree(h->hRec);
     if (h->hCtl) (void)hipHostFree(h->hCtl);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
