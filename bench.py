@@ -29,6 +29,7 @@ torch.distributed.run already set RANK / WORLD_SIZE; the control plane is
 pyratslam_amd.dist (TCP, no PyTorch), the data path RCCL.
 """
 import argparse
+import ctypes
 import json
 import os
 import platform
@@ -386,6 +387,17 @@ def bench_posecell_stress(args, d):
             'roofline': pc_roofline(ncell, 1e6 * dt / n)}
 
 
+def _near_tie_calls(net):
+    """Halo form: how many calls so far had their last step keyed by the finishing pass
+    (a cell within 2^-20 of the peak, RS_PC_DBG_HALO_AMBIG); None for other forms."""
+    if net.step_form() != 'halo':
+        return None
+    from pyratslam_amd import _lib
+    v = ctypes.c_int64(-1)
+    _lib.check(net._lib.rs_pc_debug_value(net._h, _lib.RS_PC_DBG_HALO_AMBIG, ctypes.byref(v)))
+    return int(v.value)
+
+
 def _device_us_per_step(net, od, start, n):
     """Device time per batched step: two HIP events around one whole run() of the n
     steps od[start:start + n] (no event between the launches, so nothing is added
@@ -421,6 +433,7 @@ def bench_posecells(args, d):
     for v in od[base + 16:base + 16 + args.pc_calls]:
         net.update(v)
     c1 = time.perf_counter()
+    near_ties = _near_tie_calls(net)
     dev_us = _device_us_per_step(net, od, args.pc_warmup, args.pc_steps)
     ncell = shape[0] * shape[1] * shape[2]
     finite = bool(np.isfinite(net.posecells).all())
@@ -433,6 +446,7 @@ def bench_posecells(args, d):
         'shape': list(shape),
         'steps_per_s': args.pc_steps / dt,
         'update_calls_per_s': args.pc_calls / (c1 - c0),
+        'update_near_tie_calls': near_ties,
         'us_per_step': 1e6 * dt / args.pc_steps,
         'device_us_per_step': dev_us,
         'replicas': d.world,

@@ -1495,7 +1495,14 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
             if (h->timing) RS_HIP(hipEventRecord(h->ev1, h->stream));
             h->timedScan = h->timing;
         } else {
-            const int gb = std::min(nb, VT_UP_GROUP);
+            // groups of about a quarter of the call (2 .. VT_UP_GROUP batches): the first
+            // group's upload is the only one not hidden behind a scan, and a scan launch of
+            // >= 2 batches keeps the fused launch's efficiency (RS_VT_UP_GROUP overrides)
+            static const int gb_env = [] {
+                const char* e = std::getenv("RS_VT_UP_GROUP");
+                return e ? std::atoi(e) : 0;
+            }();
+            const int gb = gb_env > 0 ? std::min(nb, gb_env) : std::min(nb, std::max(2, std::min(VT_UP_GROUP, nb / 4)));
             if (!h->ustream) {
                 RS_HIP(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
                 for (int i = 0; i < 2; ++i) {

@@ -50,6 +50,10 @@ def child(shape, calls, loop_so, mode):
     us = np.zeros(1)
     st = lib.pc_call_loop(net._h, calls, c_od.ctypes.data, us.ctypes.data)
     assert st == 0, st
+    amb = ctypes.c_int64(-1)
+    if net.step_form() == 'halo':
+        from pyratslam_amd import _lib
+        _lib.check(net._lib.rs_pc_debug_value(net._h, _lib.RS_PC_DBG_HALO_AMBIG, ctypes.byref(amb)))
     net.set_profiling(True, per_kernel=False)
     dev = []
     for v in od[3 * calls:3 * calls + 200]:
@@ -58,7 +62,8 @@ def child(shape, calls, loop_so, mode):
     net.set_profiling(False)
     dev.sort()
     print(json.dumps({'form': net.step_form(), 'shape': list(shape), 'python_update_us': 1e6 * py,
-                      'c_loop_update_us': float(us[0]), 'device_span_us_median': dev[len(dev) // 2]}),
+                      'c_loop_update_us': float(us[0]), 'device_span_us_median': dev[len(dev) // 2],
+                      'near_tie_calls': amb.value}),
           flush=True)
 
 
