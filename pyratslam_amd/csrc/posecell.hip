@@ -2030,6 +2030,7 @@ constexpr float HF_NEAR = 0x1p-20f;           // relative margin of a possible r
 // scaled state (a cell within HF_NEAR of the maximum): never a valid key (a key's low
 // word is ~lin >= 2, lin < X*Y*TH < 2^32 - 1, rs_pc_create)
 constexpr unsigned long long RES_AMBIG = 1ull;
+constexpr unsigned long long REC_SET = 1ull << 63;   // a record's count word: REC_SET | count
 
 // One step's control, a kernel argument (formed on the host by make_ctl_halo).
 struct PcCtlHalo {
@@ -2538,7 +2539,9 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             // one 16-byte store: the record may live in pinned host memory (a one-step
             // call, pc_run_halo), where each store is a PCIe write
             typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
-            *reinterpret_cast<u2*>(rec + 2 * blockIdx.x) = u2{m, (unsigned long long)cnt};
+            // (the count word carries REC_SET, so that neither word of a landed record is
+            // zero: the host polling a one-step call's records waits for both)
+            *reinterpret_cast<u2*>(rec + 2 * blockIdx.x) = u2{m, REC_SET | (unsigned long long)cnt};
         }
     }
     if (tid == 0) {
@@ -2672,7 +2675,7 @@ __global__ __launch_bounds__(64) void pc_halo_export(const unsigned long long* _
             bool amb = false;
             for (int b = lane; b < nrec; b += 64) {
                 const unsigned long long kb = rec[2 * b];
-                amb |= kb == m ? rec[2 * b + 1] > 1ull : __uint_as_float((unsigned)(kb >> 32)) >= thr;
+                amb |= kb == m ? (rec[2 * b + 1] & ~REC_SET) > 1ull : __uint_as_float((unsigned)(kb >> 32)) >= thr;
             }
             amb = __ballot(amb) != 0ull;
             if (!exact && amb) m = RES_AMBIG;
@@ -3106,7 +3109,7 @@ inline StepOut step_out(const rs_pc* h, int s) {
 unsigned long long halo_key_from_records(const unsigned long long* rec, int nrec) {
     unsigned long long m = 0ull;
     for (int b = 0; b < nrec; ++b) {
-        if (rec[2 * b] == 0ull) return RES_NONE;
+        if (rec[2 * b] == 0ull || rec[2 * b + 1] == 0ull) return RES_NONE;
         m = std::max(m, rec[2 * b]);
     }
     auto val = [](unsigned long long k) {
@@ -3119,7 +3122,7 @@ unsigned long long halo_key_from_records(const unsigned long long* rec, int nrec
     if (!(gv > 0.f) || std::isinf(gv) || std::isnan(gv)) return m;   // 0, inf, NaN maxima are exact
     for (int b = 0; b < nrec; ++b) {
         const unsigned long long kb = rec[2 * b];
-        if (kb == m ? rec[2 * b + 1] > 1ull : val(kb) >= thr) return RES_AMBIG;
+        if (kb == m ? (rec[2 * b + 1] & ~REC_SET) > 1ull : val(kb) >= thr) return RES_AMBIG;
     }
     return m;
 }
@@ -3159,15 +3162,21 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (pk) RS_TRY(pc_ensure_events(h, (size_t)2 * n + 2));
     for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
     // RS_PC_HALO_SETTLE=1: every call ends normalised (the round-4 sequence, A/B);
-    // RS_PC_HALO_EXPORT=last: that finishing kernel's last block exports the keys;
-    // RS_PC_HALO_FENCE=1: that hand-off fenced
+    // RS_PC_HALO_EXPORT=kernel: the finishing kernel's keys exported by a separate launch
+    // instead of its last block; RS_PC_HALO_FENCE=1: that hand-off fenced;
+    // RS_PC_HALO_POLL=0: a one-step call waits for the kernel's completion signal instead
+    // of returning once every block's record has reached host memory (below)
     static const bool settle_env = [] {
         const char* e = std::getenv("RS_PC_HALO_SETTLE");
         return e && std::strcmp(e, "1") == 0;
     }();
-    static const bool export_last = [] {
+    static const bool export_last = [] {   // (node step, eager: 28.2 vs 29.3 us at 21x21x36, round 5)
         const char* e = std::getenv("RS_PC_HALO_EXPORT");
-        return e && std::strcmp(e, "last") == 0;
+        return !(e && std::strcmp(e, "kernel") == 0);
+    }();
+    static const bool poll_env = [] {
+        const char* e = std::getenv("RS_PC_HALO_POLL");
+        return !(e && std::strcmp(e, "0") == 0);
     }();
     static const int fence = [] {
         const char* e = std::getenv("RS_PC_HALO_FENCE");
@@ -3239,7 +3248,27 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     h->dbgSkipExport = false;
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n + 1], h->stream));
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
-    RS_HIP(hipStreamSynchronize(h->stream));
+    // A one-step call returns as soon as every block's record has reached the pinned host
+    // array, without waiting for the kernel's completion signal and the host's wake-up
+    // (update() at 64x64x36: 22.5-24.3 -> 16.8-18.9 us, tools/pc_ab.py --mode update,
+    // round 5).  What makes the early return safe: the host reads nothing but the
+    // records, each block's last store (one 16-byte store, both words non-zero, checked
+    // after the host zeroed them); the state and every other result stay on the device,
+    // and every later access to them -- the next step, a read, inject, get_max,
+    // settle -- is a launch or copy ordered on this stream behind the kernel (the
+    // library's volume reads into pinned memory synchronise the stream themselves).
+    // A spin that runs out (a slow or faulted kernel) falls back to the stream
+    // synchronisation, which returns any error.
+    bool polled = false;
+    if (host_rec && !skipped && poll_env && !h->profiling) {
+        const volatile unsigned long long* r = h->hRec;
+        const int nr = (int)grid.x;
+        int b = 0;
+        for (long spin = 0; spin < 4000000 && b < nr; ++spin)
+            while (b < nr && r[2 * b] != 0ull && r[2 * b + 1] != 0ull) ++b;
+        polled = b == nr;
+    }
+    if (!polled) RS_HIP(hipStreamSynchronize(h->stream));
     if (host_rec && !skipped) h->hRes[n - 1] = halo_key_from_records(h->hRec, (int)grid.x);
     if (lazy && !skipped && h->hRes[n - 1] == RES_AMBIG) {
         // a cell within HF_NEAR of the last step's peak: key the normalised state itself
