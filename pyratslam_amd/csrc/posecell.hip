@@ -3103,6 +3103,20 @@ inline StepOut step_out(const rs_pc* h, int s) {
     return step_out(h->dRes, h->dArgV, h->dArgI, h->esz, h->nPathBlocks, s);
 }
 
+// Wait for a call's result words (pinned host memory, each one 8-byte system-scope store
+// by the call's last kernel) instead of the stream's completion signal: a bounded spin
+// that returns true once every word of steps [s0, s1) holds a key, false when it runs
+// out (the caller then synchronises the stream, which returns any error).  Safe for the
+// same reason as the halo form's record polling (pc_run_halo): the host reads nothing
+// else the call wrote, and every later device access is ordered on the stream.
+bool pc_poll_words(const rs_pc* h, int s0, int s1) {
+    const volatile unsigned long long* w = h->hRes;
+    int s = s0;
+    for (long spin = 0; spin < 4000000 && s < s1; ++spin)
+        while (s < s1 && w[s] != RES_NONE) ++s;
+    return s == s1;
+}
+
 // pc_halo_export's last-step rule on the host, over records in pinned host memory: the
 // largest key, or RES_AMBIG when another cell may round to the same scaled value; RES_NONE
 // when a block's record is missing (a record's key is never 0).
@@ -3260,13 +3274,17 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     // A spin that runs out (a slow or faulted kernel) falls back to the stream
     // synchronisation, which returns any error.
     bool polled = false;
-    if (host_rec && !skipped && poll_env && !h->profiling) {
-        const volatile unsigned long long* r = h->hRec;
-        const int nr = (int)grid.x;
-        int b = 0;
-        for (long spin = 0; spin < 4000000 && b < nr; ++spin)
-            while (b < nr && r[2 * b] != 0ull && r[2 * b + 1] != 0ull) ++b;
-        polled = b == nr;
+    if (lazy && !skipped && poll_env && !h->profiling) {
+        if (host_rec) {
+            const volatile unsigned long long* r = h->hRec;
+            const int nr = (int)grid.x;
+            int b = 0;
+            for (long spin = 0; spin < 4000000 && b < nr; ++spin)
+                while (b < nr && r[2 * b] != 0ull && r[2 * b + 1] != 0ull) ++b;
+            polled = b == nr;
+        } else {
+            polled = pc_poll_words(h, 0, n);   // the export kernel's words
+        }
     }
     if (!polled) RS_HIP(hipStreamSynchronize(h->stream));
     if (host_rec && !skipped) h->hRes[n - 1] = halo_key_from_records(h->hRec, (int)grid.x);
@@ -3278,7 +3296,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         hipLaunchKernelGGL(pc_res_export, dim3(1), dim3(64), 0, h->stream, h->dRes + (size_t)(n - 1) * RES_SLOTS, 1,
                            h->hResDev + (n - 1));
         RS_HIP(hipGetLastError());
-        RS_HIP(hipStreamSynchronize(h->stream));
+        if (!(poll_env && pc_poll_words(h, n - 1, n))) RS_HIP(hipStreamSynchronize(h->stream));
         ++h->haloAmbig;
     }
     for (int s = 0; s < n; ++s)
@@ -3496,6 +3514,7 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         RS_HIP(hipGetLastError());
     }
     for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
+    const bool skipped = h->dbgSkipExport;
     if (!h->dbgSkipExport) {
         hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0,
                            h->stream, h->dRes, n, h->hResDev);
@@ -3513,7 +3532,16 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         RS_HIP(hipGetLastError());
     }
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
-    RS_HIP(hipStreamSynchronize(h->stream));
+    // the result words polled (pc_poll_words) unless a volume goes to host memory (the
+    // eager readback: its stores are ordered before the host only by the stream's
+    // completion), the call is profiled or the export was withheld (RS_PC_HALO_POLL=0:
+    // always the stream synchronisation)
+    static const bool poll_env = [] {
+        const char* e = std::getenv("RS_PC_HALO_POLL");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (!(poll_env && !h->exportDev && !h->profiling && !skipped && pc_poll_words(h, 0, n)))
+        RS_HIP(hipStreamSynchronize(h->stream));
     for (int s = 0; s < n; ++s)
         RS_CHECK(h->hRes[s] != RES_NONE, RS_ERR_HIP,
                  "step %d of %d: its argmax key did not reach the host result buffer after the "
