@@ -2035,6 +2035,7 @@ constexpr unsigned long long REC_SET = 1ull << 63;   // a record's count word: R
 // wait in the stream synchronisation with the CPU idle (a 4,000-step run: 9.13 polled vs
 // 9.02 us per step synchronised, tools/pc_ab.py, round 5)
 constexpr int HF_POLL_MAX = 64;
+constexpr int HF_FLAGS = 1024;   // pc_halo_finish blocks' flags in pinned host memory
 
 // One step's control, a kernel argument (formed on the host by make_ctl_halo).
 struct PcCtlHalo {
@@ -2572,7 +2573,7 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     int n4, const double* __restrict__ part,
     int npart, unsigned long long* __restrict__ slot, const unsigned long long* __restrict__ res,
     int nexp, unsigned* __restrict__ counter, unsigned long long* __restrict__ host,
-    double* __restrict__ xp, int nbytes, int fence) {
+    double* __restrict__ xp, int nbytes, int fence, unsigned* __restrict__ flag, unsigned seq) {
     __shared__ unsigned long long s_bk[4];
     __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2596,10 +2597,20 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     }
     bk = co_wave_max(bk);
     if (lane == 0) s_bk[wave] = bk;
+    // flag (an eager readback the host polls for, pc_run_halo): every wave's volume
+    // stores acknowledged before the block's barrier, then one lane's system-scope
+    // release and the block's flag -- the producer form MI355X_MICROARCH.md gives
+    // (stores, each wave's vmcnt(0), barrier, release, vmcnt(0), flag store)
+    if (flag) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         bk = max(max(s_bk[0], s_bk[1]), max(s_bk[2], s_bk[3]));
         if (slot) atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
+        if (flag) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         s_last = 0;
         if (nexp > 0) {
             // The hand-off of the keys to the block that counts last: the key is an
@@ -2923,6 +2934,9 @@ struct rs_pc {
     unsigned long long* dRec = nullptr;  // halo: the last launch's per-block (key of max U, near count)
     unsigned long long* hRec = nullptr;  // ... for a one-step call: pinned host records (hRecDev on the device)
     unsigned long long* hRecDev = nullptr;
+    unsigned* hFlag = nullptr;      // halo: pc_halo_finish's per-block flags (pinned; eager readback polls)
+    unsigned* hFlagDev = nullptr;
+    unsigned flagSeq = 0u;
     bool haloPend = false;  // halo: the state is U, unnormalised, in buffer haloCur (0 dP, 1 dQ) with
     int haloCur = 0, haloPart = 0;  // its partial sums in half haloPart of dPart (pc_halo_settle)
     long haloAmbig = 0;     // calls whose last step was keyed by the finishing pass (RES_AMBIG)
@@ -3121,6 +3135,18 @@ bool pc_poll_words(const rs_pc* h, int s0, int s1) {
     return s == s1;
 }
 
+// An eager halo call (the volume written into the caller's pinned array) polls the
+// finishing blocks' flags instead of the stream's completion when it is short and not
+// profiled; RS_PC_HALO_FLAGS=0 keeps the stream synchronisation for it.
+bool xp_poll_ok(const rs_pc* h, int n, bool poll_env) {
+    static const bool flags_env = [] {
+        const char* e = std::getenv("RS_PC_HALO_FLAGS");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return poll_env && flags_env && h->exportDev && h->hFlag && !h->profiling && !h->dbgSkipExport &&
+           n <= HF_POLL_MAX && (int)std::min<size_t>(1024, (h->n / 4 + 255) / 256) <= HF_FLAGS;
+}
+
 // pc_halo_export's last-step rule on the host, over records in pinned host memory: the
 // largest key, or RES_AMBIG when another cell may round to the same scaled value; RES_NONE
 // when a block's record is missing (a record's key is never 0).
@@ -3155,7 +3181,7 @@ int pc_halo_settle(rs_pc* h) {
     const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
     hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
                        h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
-                       nullptr, nullptr, (int)(h->n * sizeof(float)), 0);
+                       nullptr, nullptr, (int)(h->n * sizeof(float)), 0, nullptr, 0u);
     RS_HIP(hipGetLastError());
     h->haloPend = false;
     h->haloCur = 0;
@@ -3234,10 +3260,19 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     }
     const int cl = (c0 + n) & 1, pl = (p0 + n - 1) & 1;   // where the last U and its partials are
     const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
+    // an eager readback the host may poll for (per-block flags behind a system-scope release)
+    const bool flag_poll = xp_poll_ok(h, n, poll_env);
+    unsigned seq = 0u;
+    if (flag_poll) {
+        seq = ++h->flagSeq;
+        if (seq == 0u) seq = ++h->flagSeq;   // (0 is the flags' initial value)
+    }
     auto finish = [&](int nexp_own, double* xp) -> int {
+        const bool fl = flag_poll && xp != nullptr;
         hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[cl], buf[0], n4,
                            h->dPart + (size_t)pl * h->nPart, h->nPart, h->dRes + (size_t)(n - 1) * RES_SLOTS,
-                           h->dRes, nexp_own, h->dCounter, h->hResDev, xp, (int)(h->n * sizeof(float)), fence);
+                           h->dRes, nexp_own, h->dCounter, h->hResDev, xp, (int)(h->n * sizeof(float)), fence,
+                           fl ? h->hFlagDev : nullptr, seq);
         RS_HIP(hipGetLastError());
         h->haloPend = false;
         h->haloCur = 0;
@@ -3278,6 +3313,15 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     // A spin that runs out (a slow or faulted kernel) falls back to the stream
     // synchronisation, which returns any error.
     bool polled = false;
+    if (flag_poll && !lazy && !skipped) {
+        // the eager readback: every finishing block's flag (its volume slice released at
+        // system scope before it), then every step's key word
+        const volatile unsigned* f = h->hFlag;
+        int b = 0;
+        for (long spin = 0; spin < 4000000 && b < nb; ++spin)
+            while (b < nb && f[b] == seq) ++b;
+        polled = b == nb && pc_poll_words(h, 0, n);
+    }
     if (lazy && !skipped && poll_env && !h->profiling && n <= HF_POLL_MAX) {
         if (host_rec) {
             const volatile unsigned long long* r = h->hRec;
@@ -3929,6 +3973,9 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         PC_ALLOC(hipHostMalloc(&h->hRec, sizeof(unsigned long long) * 2 * h->nPart,
                                hipHostMallocMapped | hipHostMallocCoherent));
         PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hRecDev), h->hRec, 0));
+        PC_ALLOC(hipHostMalloc(&h->hFlag, sizeof(unsigned) * HF_FLAGS, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(h->hFlag, 0, sizeof(unsigned) * HF_FLAGS);
+        PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hFlagDev), h->hFlag, 0));
     }
     PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
     PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
@@ -3971,6 +4018,7 @@ int rs_pc_destroy(rs_pc* h) {
         if (p) (void)hipFree(p);
     if (h->hRes) (void)hipHostFree(h->hRes);
     if (h->hRec) (void)hipHostFree(h->hRec);
+    if (h->hFlag) (void)hipHostFree(h->hFlag);
     if (h->hCtl) (void)hipHostFree(h->hCtl);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
