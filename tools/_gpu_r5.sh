@@ -1,5 +1,7 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-bash tools/profile_r2.sh r5_v1 > gpurun_out/profile_r5_v1.log 2>&1 || { tail -20 gpurun_out/profile_r5_v1.log; exit 1; }
-tail -3 gpurun_out/profile_r5_v1.log
+rocprofv3 --list-avail > gpurun_out/pmc_avail.txt 2>&1 || true
+grep -i -E "ICACHE|IFETCH|SQC_" gpurun_out/pmc_avail.txt | head -40
+timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE --output-format csv -d gpurun_out/icache -o run -- python tools/scan_profile.py pc --shape 64,64,36 --steps 400 > gpurun_out/icache.log 2>&1; echo rc=$?
+tail -3 gpurun_out/icache.log
