@@ -900,6 +900,7 @@ struct rs_vt {
     unsigned long long* dBest = nullptr;
     unsigned long long* hBest = nullptr;  // pinned
     unsigned long long* hBestDev = nullptr;  // hBest in the device's address space
+    bool stagingBusy = false;  // copies from hSrc / hDst queued and not yet known to have run
     hipStream_t cstream = nullptr;           // rs_vt_match_stream's collective stream
     hipEvent_t evScan = nullptr, evComm = nullptr;
     hipStream_t ustream = nullptr;           // rs_vt_match_stream: host batches' upload stream
@@ -1039,7 +1040,8 @@ int vt_grow_queries(rs_vt* h, int nq) {
     RS_HIP(hipMalloc(&h->dQf, sizeof(uint2) * (size_t)h->WD * h->H * cap));
     RS_HIP(hipMalloc(&h->dQsum, sizeof(uint32_t) * cap));
     RS_HIP(hipMalloc(&h->dBest, sizeof(unsigned long long) * cap));
-    RS_HIP(hipHostMalloc(&h->hBest, sizeof(unsigned long long) * cap, hipHostMallocDefault));
+    // fine-grained (coherent): vt_fetch_keys polls the words the export kernel stores
+    RS_HIP(hipHostMalloc(&h->hBest, sizeof(unsigned long long) * cap, hipHostMallocMapped | hipHostMallocCoherent));
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hBestDev), h->hBest, 0));
     h->bestClean = h->bestPending = 0;
     h->qCap = cap;
@@ -1155,6 +1157,7 @@ int vt_store(rs_vt* h, bool cand, const uint8_t* d_raw, int n) {
     uint4* lib = cand ? h->dCand : h->dLib;
     RS_HIP(hipMemcpyAsync(h->dSrc, h->hSrc, sizeof(int32_t) * n, hipMemcpyHostToDevice, h->stream));
     RS_HIP(hipMemcpyAsync(h->dDst, h->hDst, sizeof(int64_t) * n, hipMemcpyHostToDevice, h->stream));
+    h->stagingBusy = true;
     const int64_t total = (int64_t)n * h->WD * h->HQ;
     const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
     hipLaunchKernelGGL(vt_store_kernel, dim3(grid), dim3(256), 0, h->stream, d_raw, h->dSrc,
@@ -1262,9 +1265,43 @@ int vt_launch_scan(rs_vt* h, bool cand, int64_t count, int nq, ScanOut out, int 
     return RS_OK;
 }
 
+// The host waits for a call's keys by polling them (pinned, fine-grained; each key one
+// 8-byte system-scope store by vt_keys_export, the call's last kernel) instead of the
+// stream's completion signal and its own wake-up: the host reads nothing else the call
+// wrote, and every later device access is ordered on the stream (the pinned staging
+// arrays a call's copies read are guarded by vt_staging_idle).  A spin that runs out
+// falls back to the stream synchronisation.  RS_VT_POLL=0: always synchronise.
+constexpr unsigned long long KEY_PENDING = 0xFFFFFFFF00000000ull;  // score 2^32-1: never a key
+constexpr int VT_POLL_MAX = 4096;
+bool vt_poll_env() {
+    static const bool on = [] {
+        const char* e = std::getenv("RS_VT_POLL");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+bool vt_poll_keys(const unsigned long long* w_, int n) {
+    const volatile unsigned long long* w = w_;
+    int i = 0;
+    for (long spin = 0; spin < 4000000 && i < n; ++spin)
+        while (i < n && w[i] != KEY_PENDING) ++i;
+    return i == n;
+}
+
+// The pinned staging arrays hSrc / hDst are read by asynchronous copies (vt_store):
+// before the host writes or reallocates them again, those copies must have run.
+int vt_staging_idle(rs_vt* h) {
+    if (h->stagingBusy) {
+        RS_HIP(hipStreamSynchronize(h->stream));
+        h->stagingBusy = false;
+    }
+    return RS_OK;
+}
+
 int vt_append_staged(rs_vt* h, const std::vector<std::pair<int, int64_t>>& news) {
     // news: (staged query index, global index) in order
     int mine = 0;
+    RS_TRY(vt_staging_idle(h));
     RS_TRY(vt_grow_index(h, (int)news.size() + 1));
     const int64_t new_count = h->count + (int64_t)news.size();
     RS_TRY(vt_grow_lib(h, local_count_of(h, new_count)));
@@ -1341,6 +1378,7 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
     std::vector<int> cpos(nq, -1);
     int64_t ldm = 0;
     if (!cand.empty() && cand.front() < nq - 1) {
+        RS_TRY(vt_staging_idle(h));
         const int64_t C = (int64_t)cand.size();
         RS_TRY(vt_grow_cand(h, (int64_t)rs::round_up((size_t)C, 64)));
         RS_TRY(vt_grow_index(h, (int)C));
@@ -1357,6 +1395,7 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
         RS_HIP(hipMemcpyAsync(h->hMat, h->dMat, sizeof(uint32_t) * ldm * nq, hipMemcpyDeviceToHost,
                               h->stream));
         RS_HIP(hipStreamSynchronize(h->stream));
+        h->stagingBusy = false;
     }
     std::vector<std::pair<int, int64_t>> news;
     for (int i = 0; i < nq; ++i) {
@@ -1379,8 +1418,7 @@ int vt_resolve_impl(rs_vt* h, int nq, const unsigned long long* keys, int mode,
         }
         if (best_score) best_score[i] = k == NO_KEY ? UINT64_MAX : (k >> 32);
     }
-    RS_TRY(vt_append_staged(h, news));
-    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_TRY(vt_append_staged(h, news));   // (its copies guarded by vt_staging_idle, not a sync)
     return RS_OK;
 }
 
@@ -1393,10 +1431,16 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
         RS_CHECK(r == ncclSuccess, RS_ERR_RCCL, "ncclAllReduce(min) failed: %s",
                  ncclGetErrorString(r));
     }
+    const bool poll = vt_poll_env() && !h->timedScan && nq <= VT_POLL_MAX;
+    if (poll)
+        for (int i = 0; i < nq; ++i) h->hBest[i] = KEY_PENDING;
     hipLaunchKernelGGL(vt_keys_export, dim3((nq + 255) / 256 < 64 ? (nq + 255) / 256 : 64), dim3(256), 0,
                        h->stream, h->dBest, nq, h->hBestDev);
     RS_HIP(hipGetLastError());
-    RS_HIP(hipStreamSynchronize(h->stream));
+    if (!(poll && vt_poll_keys(h->hBest, nq))) {
+        RS_HIP(hipStreamSynchronize(h->stream));
+        h->stagingBusy = false;
+    }
     h->bestClean = h->bestPending;
     if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     return RS_OK;
@@ -1728,8 +1772,7 @@ int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
     std::vector<std::pair<int, int64_t>> news;
     news.reserve(n);
     for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
-    RS_TRY(vt_append_staged(h, news));
-    RS_HIP(hipStreamSynchronize(h->stream));
+    RS_TRY(vt_append_staged(h, news));   // (its copies guarded by vt_staging_idle, not a sync)
     return RS_OK;
 }
 

@@ -1,7 +1,6 @@
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-rocprofv3 --list-avail > gpurun_out/pmc_avail.txt 2>&1 || true
-grep -i -E "ICACHE|IFETCH|SQC_" gpurun_out/pmc_avail.txt | head -40
-timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE --output-format csv -d gpurun_out/icache -o run -- python tools/scan_profile.py pc --shape 64,64,36 --steps 400 > gpurun_out/icache.log 2>&1; echo rc=$?
-tail -3 gpurun_out/icache.log
+timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu > gpurun_out/gputest_r5_v7.log 2>&1 || { tail -60 gpurun_out/gputest_r5_v7.log; exit 1; }
+tail -2 gpurun_out/gputest_r5_v7.log
+for p in 1 0 1 0; do RS_VT_POLL=$p timeout -k 10 300 python -u bench.py --library-total 0 --no-pc-stress --no-cpu-baseline --pc-calls 2000 --node-calls 300 --steps 5 > gpurun_out/bvp_$p.json 2>/dev/null || exit 1; python3 -c "import json;d=json.loads(open('gpurun_out/bvp_$p.json').read().strip().splitlines()[-1]);r=d['replay'];print('poll $p', round(d['value']/1e9,3), {k: round(v) for k,v in r.items() if k.endswith('per_s')}, r.get('publish',{}).get('messages_per_s'))"; done
