@@ -2541,12 +2541,13 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             int cnt = 0;
 #pragma unroll
             for (int w = 0; w < HF_NW; ++w) cnt += s_cnt[w];
-            // one 16-byte store: the record may live in pinned host memory (a one-step
-            // call, pc_run_halo), where each store is a PCIe write
-            typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
-            // (the count word carries REC_SET, so that neither word of a landed record is
-            // zero: the host polling a one-step call's records waits for both)
-            *reinterpret_cast<u2*>(rec + 2 * blockIdx.x) = u2{m, REC_SET | (unsigned long long)cnt};
+            // the record may live in pinned host memory (a one-step call, pc_run_halo,
+            // whose host polls it): two system-scope stores, written through to memory;
+            // the count word carries REC_SET, so that neither word of a landed record is
+            // zero and the host waits for both
+            __hip_atomic_store(rec + 2 * blockIdx.x, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(rec + 2 * blockIdx.x + 1, REC_SET | (unsigned long long)cnt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     if (tid == 0) {
