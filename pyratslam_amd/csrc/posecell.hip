@@ -2016,15 +2016,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 constexpr int HF_T = 4;                       // tile: HF_T x HF_T cells through all layers
 constexpr int HF_W = HF_T + 4 * HALF;         // 16: a layer's excitation window
 constexpr int HF_Q = HF_T + 2 * HALF;         // 10: a layer's excited (Q) window
-#ifndef PC_HF_NW
-#define PC_HF_NW 9
-#endif
-// 9 waves (576 threads: one task per (layer, window row) at TH = 36): 8 run the theta pass
-// (4 window-row groups x 2 layer halves) while the 9th keys the entering state; 12
-// waves (PC_HF_NW=12, A/B): 4 row groups x 3 layer thirds, the keys after the pass
-constexpr int HF_NW = PC_HF_NW, HF_NT = 64 * HF_NW;
-constexpr int HF_TW = HF_NW >= 12 ? 12 : 8;    // waves of the theta pass
-static_assert(HF_NW == 9 || HF_NW == 12, "instantiated block shapes");
+constexpr int HF_NW = 9, HF_NT = 64 * HF_NW;  // 576 threads: one task per (layer, window row) at TH = 36
 constexpr int HF_TH = 36;                     // the theta extent instantiated (configs[1], the ROS node)
 constexpr int HF_UMAX = 22 * 22;              // union cells staged by LDS-DMA (|shifts| spread <= 6)
 // theta-pass windows, (e, i) pairs [j][rx][ry], row pitch 18 pairs: the y pass's 16-byte
@@ -2205,8 +2197,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
             co_lds_barrier();
         }
-        if (wave < HF_TW) {
-            constexpr int JH = TH / (HF_TW / 4), PF = 3;
+        if (wave < 8) {
+            constexpr int JH = TH / 2, PF = 3;
             const int rx = 4 * (wave & 3) + (lane >> 4), ry = lane & 15;
             const int loff = (lsx * UH + lsy) * TH;   // lane L: layer L's window place in the union
             const int cbase = (rx * UH + ry) * TH;
@@ -2276,22 +2268,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 }
             };
             if (wave < 4) run(std::integral_constant<int, 0>{});
-            else if (HF_TW == 8 || wave < 8) run(std::integral_constant<int, 1>{});
-            else if constexpr (HF_TW == 12) run(std::integral_constant<int, 2>{});
-        }
-        if (HF_TW == 12 && want_key) {
-            // every thread keys at most one value of the own tile's entering state (the
-            // union image is read until the barrier below)
-            for (int t = tid; t < HF_T * HF_T * TH; t += HF_NT) {
-                const int cell = t / TH, q = t - cell * TH, i = cell >> 2, jc = cell & 3;
-                int cu = co_wrap(2 * HALF - cux, X) + i, cv = co_wrap(2 * HALF - cuy, Y) + jc;
-                cu -= cu >= X ? X : 0;
-                cv -= cv >= Y ? Y : 0;
-                if (i < tw && jc < tht && cu < UW && cv < UH)
-                    bk = max(bk, argmax_key(s_b[(cu * UH + cv) * TH + q] * nrm.r,
-                                            ((unsigned)(x0 + i) * Y + (y0 + jc)) * TH + q));
-            }
-        } else if (wave >= HF_TW && want_key) {
+            else run(std::integral_constant<int, 1>{});
+        } else if (want_key) {
             // wave 8: the argmax of the state entering the step over the own tile (lane:
             // cell lane & 15, quads lane >> 4 + 4 m)
             const int i = (lane & 15) >> 2, jc = lane & 3;
