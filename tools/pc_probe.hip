@@ -78,6 +78,9 @@ int main(int argc, char** argv) {
         return 1;
     }
     rs_pc_inject(h, 1.0, X / 2, Y / 2, TH / 2);
+    // the halo form's last step of a call would also write its per-block records (a
+    // one-call-end extra): settle every call, so the stamped last step is a batch step
+    rs_pc_debug(h, RS_PC_DBG_HALO_SETTLE);
     unsigned long long* dbg;
     constexpr int NKID = 16;  // stamp slots: kernel id x 4096 blocks x 8 stamps
     const size_t ndbg = (size_t)NKID * 4096 * 8;
