@@ -3140,13 +3140,33 @@ bool pc_poll_words(const rs_pc* h, int s0, int s1) {
 // An eager halo call (the volume written into the caller's pinned array) polls the
 // finishing blocks' flags instead of the stream's completion when it is short and not
 // profiled; RS_PC_HALO_FLAGS=0 keeps the stream synchronisation for it.
-bool xp_poll_ok(const rs_pc* h, int n, bool poll_env) {
-    static const bool flags_env = [] {
+bool halo_poll_env() {
+    static const bool on = [] {
+        const char* e = std::getenv("RS_PC_HALO_POLL");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+bool halo_flags_env() {
+    static const bool on = [] {
         const char* e = std::getenv("RS_PC_HALO_FLAGS");
         return !(e && std::strcmp(e, "0") == 0);
     }();
-    return poll_env && flags_env && h->exportDev && h->hFlag && !h->profiling && !h->dbgSkipExport &&
+    return on;
+}
+bool xp_poll_ok(const rs_pc* h, int n, bool poll_env) {
+    return poll_env && halo_flags_env() && h->exportDev && h->hFlag && !h->profiling && !h->dbgSkipExport &&
            n <= HF_POLL_MAX && (int)std::min<size_t>(1024, (h->n / 4 + 255) / 256) <= HF_FLAGS;
+}
+
+// Spin until pc_halo_finish's nb blocks have each stored flag value seq (bounded; false
+// when the spin runs out and the caller must synchronise the stream instead).
+bool pc_poll_flags(const rs_pc* h, int nb, unsigned seq) {
+    const volatile unsigned* f = h->hFlag;
+    int b = 0;
+    for (long spin = 0; spin < 4000000 && b < nb; ++spin)
+        while (b < nb && f[b] == seq) ++b;
+    return b == nb;
 }
 
 // pc_halo_export's last-step rule on the host, over records in pinned host memory: the
@@ -3190,6 +3210,37 @@ int pc_halo_settle(rs_pc* h) {
     return RS_OK;
 }
 
+// A volume read of a state a halo call left unnormalised (the ROS node's `.posecells`
+// after update()): the finishing kernel normalises the state and writes the float64
+// C-order volume into the pinned destination in the same pass (the eager readback's
+// kernel: one launch in place of the settle and the export kernel), and the host waits
+// for its blocks' flags -- each released at system scope after the block's volume
+// stores -- instead of the stream's completion (RS_PC_HALO_POLL=0 or RS_PC_HALO_FLAGS=0:
+// the stream synchronisation).  The host reads only what this kernel wrote, so the
+// early return is safe as the eager call's is (pc_run_halo).  *done is false when no
+// state is pending (the caller exports as usual).
+int pc_halo_settle_read(rs_pc* h, double* xp_dev, bool* done) {
+    *done = false;
+    if (!h->haloPend) return RS_OK;
+    float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
+    const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
+    const bool fl = halo_poll_env() && halo_flags_env() && h->hFlag && !h->profiling && nb <= HF_FLAGS;
+    unsigned seq = 0u;
+    if (fl) {
+        seq = ++h->flagSeq;
+        if (seq == 0u) seq = ++h->flagSeq;   // (0 is the flags' initial value)
+    }
+    hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
+                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
+                       nullptr, xp_dev, (int)(h->n * sizeof(float)), 0, fl ? h->hFlagDev : nullptr, seq);
+    RS_HIP(hipGetLastError());
+    h->haloPend = false;
+    h->haloCur = 0;
+    if (!(fl && pc_poll_flags(h, nb, seq))) RS_HIP(hipStreamSynchronize(h->stream));
+    *done = true;
+    return RS_OK;
+}
+
 // n steps of the halo form: one launch each (step s reads the state in one buffer,
 // scaled by the partials of the step before, and writes U into the other; the partial
 // sums ping-pong between the two halves of dPart).  Then, by default, the call ends with
@@ -3220,10 +3271,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         const char* e = std::getenv("RS_PC_HALO_EXPORT");
         return !(e && std::strcmp(e, "kernel") == 0);
     }();
-    static const bool poll_env = [] {
-        const char* e = std::getenv("RS_PC_HALO_POLL");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
+    const bool poll_env = halo_poll_env();
     static const int fence = [] {
         const char* e = std::getenv("RS_PC_HALO_FENCE");
         return e && std::strcmp(e, "1") == 0 ? 1 : 0;
@@ -3318,11 +3366,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (flag_poll && !lazy && !skipped) {
         // the eager readback: every finishing block's flag (its volume slice released at
         // system scope before it), then every step's key word
-        const volatile unsigned* f = h->hFlag;
-        int b = 0;
-        for (long spin = 0; spin < 4000000 && b < nb; ++spin)
-            while (b < nb && f[b] == seq) ++b;
-        polled = b == nb && pc_poll_words(h, 0, n);
+        polled = pc_poll_flags(h, nb, seq) && pc_poll_words(h, 0, n);
     }
     if (lazy && !skipped && poll_env && !h->profiling && n <= HF_POLL_MAX) {
         if (host_rec) {
@@ -4240,7 +4284,6 @@ int rs_pc_read(rs_pc* h, double* host) {
     rs::clear_error();
     RS_CHECK(h && host, RS_ERR_ARG, "null argument");
     RS_HIP(hipSetDevice(h->device));
-    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     // The export kernel writes the float64 C-order volume straight into pinned host
     // memory (one launch, no copy engine), then the host copies it into the caller's
     // array; RS_PC_READ=dma exports to HBM and copies with hipMemcpyAsync instead.
@@ -4252,6 +4295,15 @@ int rs_pc_read(rs_pc* h, double* host) {
         RS_HIP(hipHostMalloc(&h->hRead, sizeof(double) * h->n, hipHostMallocMapped | hipHostMallocCoherent));
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hReadDev), h->hRead, 0));
     }
+    if (!dma) {
+        bool done = false;
+        RS_TRY(pc_halo_settle_read(h, h->hReadDev, &done));
+        if (done) {
+            std::memcpy(host, h->hRead, sizeof(double) * h->n);
+            return RS_OK;
+        }
+    }
+    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     double* dst = dma ? h->dTmp : h->hReadDev;
     const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
     if (h->prec == RS_PREC_F32)
@@ -4272,9 +4324,11 @@ int rs_pc_read_pinned(rs_pc* h, double* pinned) {
     RS_CHECK(h && pinned, RS_ERR_ARG, "null argument");
     RS_CHECK(reinterpret_cast<uintptr_t>(pinned) % 16 == 0, RS_ERR_ARG, "pinned buffer not 16-byte aligned");
     RS_HIP(hipSetDevice(h->device));
-    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
     double* dst = nullptr;
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), pinned, 0));
+    bool done = false;
+    RS_TRY(pc_halo_settle_read(h, dst, &done));   // (halo: a pending state, settled as it is read)
+    if (done) return RS_OK;
     const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
     if (h->prec == RS_PREC_F32)
         hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,

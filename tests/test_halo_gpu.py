@@ -347,6 +347,41 @@ def test_unnormalised_call_end_equals_settled(halo, shape):
     assert ambig_calls(a) == 0 and ambig_calls(b) == 0
 
 
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36)])
+def test_read_of_pending_state_settles_in_one_pass(halo, shape):
+    """The ROS node's step: update() then a read of the volume.  The read of a state a
+    call left unnormalised normalises it and writes the float64 volume in one pass
+    (pc_halo_settle_read: the finishing kernel with the volume, its blocks' flags
+    polled).  Against a handle that settles every call: bit-identical volumes through
+    the pinned read (`.posecells`) and the copying read (rs_pc_read); a second read of
+    the now settled state (the export kernel) gives the same bytes; the next update(),
+    inject and get_pc_max continue from the settled state."""
+    from pyratslam_amd import _lib
+    od = odometry(24, 77)
+    a, b = halo(shape), halo(shape)
+    _lib.check(b._lib.rs_pc_debug(b._h, _lib.RS_PC_DBG_HALO_SETTLE))
+    loc = tuple(x // 3 for x in shape)
+    for n in (a, b):
+        n.inject(1, loc)
+    buf = np.empty(shape)
+    for i, v in enumerate(od):
+        assert a.update(v) == b.update(v), i
+        want = b.posecells
+        if i % 3 == 2:
+            _lib.check(a._lib.rs_pc_read(a._h, _lib.ptr(buf, ctypes.c_double)))
+            got = buf.copy()
+        else:
+            got = a.posecells
+        assert np.array_equal(got, want), i
+        assert np.array_equal(a.posecells, got), i      # settled: the export kernel
+        if i == 10:
+            for n in (a, b):
+                n.inject(0.25, (1, 2, 3))
+            assert a.get_pc_max() == b.get_pc_max()
+    assert a.get_pc_max() == own_argmax(a)[0] == own_argmax(b)[0]
+    assert ambig_calls(a) == 0
+
+
 def test_halo_refused_beyond_16bit_union_fields(pcn, monkeypatch):
     """The union's origin and extent travel to the kernel as 16-bit fields
     (make_ctl_halo / hf_pack): a grid with X or Y beyond 32767 is refused by the halo
