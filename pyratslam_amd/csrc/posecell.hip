@@ -2831,9 +2831,12 @@ __global__ void pc_export_kernel(const T* __restrict__ P, double* __restrict__ o
 // The same export with 16-byte stores (two consecutive cells per thread): a wave's
 // stores are 1 KiB contiguous, the unit host writes over PCIe favour.  out is
 // 16-byte aligned (rs_host_alloc / hipMalloc); an odd last cell goes alone.
+// flag (host memory the host polls instead of the stream's completion, pc_poll_flags):
+// every wave's volume stores acknowledged, the block's barrier, one lane's system-scope
+// release, then the block's flag = seq -- the producer form of pc_halo_finish.
 template <typename T>
 __global__ void pc_export2_kernel(const T* __restrict__ P, double* __restrict__ out, int X, int Y,
-                                  int TH, int thfast) {
+                                  int TH, int thfast, unsigned* __restrict__ flag, unsigned seq) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     const size_t n = (size_t)X * Y * TH, n2 = n / 2;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
@@ -2845,6 +2848,15 @@ __global__ void pc_export2_kernel(const T* __restrict__ P, double* __restrict__ 
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
         out[n - 1] = (double)P[thfast ? n - 1 : pc_layer_major(n - 1, X, Y, TH)];
+    if (flag) {   // (kernel argument: uniform)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flag + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 template <typename T>
@@ -3169,6 +3181,28 @@ bool pc_poll_flags(const rs_pc* h, int nb, unsigned seq) {
     return b == nb;
 }
 
+// The next flag value of a volume-writing launch the host will poll (0 is the flags'
+// initial value, never a live one), and whether a launch of nb blocks may be polled.
+unsigned pc_next_seq(rs_pc* h) {
+    unsigned seq = ++h->flagSeq;
+    if (seq == 0u) seq = ++h->flagSeq;
+    return seq;
+}
+bool pc_flags_ok(const rs_pc* h, int nb) {
+    return halo_poll_env() && halo_flags_env() && h->hFlag && !h->profiling && nb <= HF_FLAGS;
+}
+// The export kernel's grid when its flags are polled: at most 128 blocks, each thread
+// storing a few 16-byte pieces (fewer blocks, fewer flags; 64x64x36 rows-form read 32-36
+// us at 32-128 blocks against 36-37 at 289, within the boxes' spread; RS_PC_XFLAG_NB
+// overrides, tools/node_step.py, round 5)
+int pc_xflag_nb(int nb) {
+    static const int cap = [] {
+        const char* e = std::getenv("RS_PC_XFLAG_NB");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 128;
+    }();
+    return std::min(nb, cap);
+}
+
 // pc_halo_export's last-step rule on the host, over records in pinned host memory: the
 // largest key, or RES_AMBIG when another cell may round to the same scaled value; RES_NONE
 // when a block's record is missing (a record's key is never 0).
@@ -3224,12 +3258,8 @@ int pc_halo_settle_read(rs_pc* h, double* xp_dev, bool* done) {
     if (!h->haloPend) return RS_OK;
     float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
     const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
-    const bool fl = halo_poll_env() && halo_flags_env() && h->hFlag && !h->profiling && nb <= HF_FLAGS;
-    unsigned seq = 0u;
-    if (fl) {
-        seq = ++h->flagSeq;
-        if (seq == 0u) seq = ++h->flagSeq;   // (0 is the flags' initial value)
-    }
+    const bool fl = pc_flags_ok(h, nb);
+    const unsigned seq = fl ? pc_next_seq(h) : 0u;
     hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
                        h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
                        nullptr, xp_dev, (int)(h->n * sizeof(float)), 0, fl ? h->hFlagDev : nullptr, seq);
@@ -3312,11 +3342,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
     // an eager readback the host may poll for (per-block flags behind a system-scope release)
     const bool flag_poll = xp_poll_ok(h, n, poll_env);
-    unsigned seq = 0u;
-    if (flag_poll) {
-        seq = ++h->flagSeq;
-        if (seq == 0u) seq = ++h->flagSeq;   // (0 is the flags' initial value)
-    }
+    const unsigned seq = flag_poll ? pc_next_seq(h) : 0u;
     auto finish = [&](int nexp_own, double* xp) -> int {
         const bool fl = flag_poll && xp != nullptr;
         hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[cl], buf[0], n4,
@@ -3615,27 +3641,35 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
         RS_HIP(hipGetLastError());
     }
     h->dbgSkipExport = false;
-    if (h->exportDev) {  // the volume after the last step, into the caller's pinned array
-        const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
+    // the volume after the last step, into the caller's pinned array (the eager
+    // readback), its blocks' flags polled when the call may return early
+    const bool may_poll = halo_poll_env() && !h->profiling && !skipped && n <= HF_POLL_MAX;
+    int xnb = 0;
+    unsigned seq = 0u;
+    if (h->exportDev) {
+        xnb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
+        const bool fl = may_poll && pc_flags_ok(h, xnb);
+        if (fl) xnb = pc_xflag_nb(xnb);
+        seq = fl ? pc_next_seq(h) : 0u;
+        unsigned* flag = fl ? h->hFlagDev : nullptr;
         if (h->prec == RS_PREC_F32)
-            hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const float*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h));
+            hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(xnb), dim3(NT), 0, h->stream,
+                               static_cast<const float*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h),
+                               flag, seq);
         else
-            hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const double*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h));
+            hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(xnb), dim3(NT), 0, h->stream,
+                               static_cast<const double*>(h->dP), h->exportDev, h->X, h->Y, h->TH, (int)pc_thfast(h),
+                               flag, seq);
         RS_HIP(hipGetLastError());
     }
     if (h->profiling) RS_HIP(hipEventRecord(h->ev1, h->stream));
-    // the result words polled (pc_poll_words) unless a volume goes to host memory (the
-    // eager readback: its stores are ordered before the host only by the stream's
-    // completion), the call is profiled or the export was withheld (RS_PC_HALO_POLL=0:
-    // always the stream synchronisation)
-    static const bool poll_env = [] {
-        const char* e = std::getenv("RS_PC_HALO_POLL");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    if (!(poll_env && !h->exportDev && !h->profiling && !skipped && n <= HF_POLL_MAX && pc_poll_words(h, 0, n)))
-        RS_HIP(hipStreamSynchronize(h->stream));
+    // the result words polled (pc_poll_words), and with an eager readback the volume's
+    // flags first (each block's stores released at system scope before its flag), unless
+    // the call is profiled, long or its export was withheld (RS_PC_HALO_POLL=0: always the
+    // stream synchronisation; RS_PC_HALO_FLAGS=0: for an eager readback)
+    const bool polled = may_poll && (h->exportDev ? seq != 0u && pc_poll_flags(h, xnb, seq) : true) &&
+                        pc_poll_words(h, 0, n);
+    if (!polled) RS_HIP(hipStreamSynchronize(h->stream));
     for (int s = 0; s < n; ++s)
         RS_CHECK(h->hRes[s] != RES_NONE, RS_ERR_HIP,
                  "step %d of %d: its argmax key did not reach the host result buffer after the "
@@ -4019,10 +4053,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
         PC_ALLOC(hipHostMalloc(&h->hRec, sizeof(unsigned long long) * 2 * h->nPart,
                                hipHostMallocMapped | hipHostMallocCoherent));
         PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hRecDev), h->hRec, 0));
-        PC_ALLOC(hipHostMalloc(&h->hFlag, sizeof(unsigned) * HF_FLAGS, hipHostMallocMapped | hipHostMallocCoherent));
-        std::memset(h->hFlag, 0, sizeof(unsigned) * HF_FLAGS);
-        PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hFlagDev), h->hFlag, 0));
     }
+    // the volume-writing kernels' per-block flags (pc_halo_finish, pc_export2_kernel)
+    PC_ALLOC(hipHostMalloc(&h->hFlag, sizeof(unsigned) * HF_FLAGS, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h->hFlag, 0, sizeof(unsigned) * HF_FLAGS);
+    PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hFlagDev), h->hFlag, 0));
     PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
     PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
@@ -4280,6 +4315,30 @@ int rs_pc_get_max(rs_pc* h, int32_t out_xyz[3]) {
     return pc_argmax_impl<double>(h, out_xyz);
 }
 
+// The float64 C-order volume into pinned host memory (dst: its device pointer) and the
+// host back once it has landed: a pending halo state settled in the same pass
+// (pc_halo_settle_read), else the export kernel; either way the writing kernel's
+// blocks' flags are polled (pc_poll_flags) where allowed, else the stream synchronised.
+int pc_read_volume(rs_pc* h, double* dst) {
+    bool done = false;
+    RS_TRY(pc_halo_settle_read(h, dst, &done));
+    if (done) return RS_OK;
+    int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
+    const bool fl = pc_flags_ok(h, nb);
+    if (fl) nb = pc_xflag_nb(nb);
+    const unsigned seq = fl ? pc_next_seq(h) : 0u;
+    unsigned* flag = fl ? h->hFlagDev : nullptr;
+    if (h->prec == RS_PREC_F32)
+        hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h), flag, seq);
+    else
+        hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
+                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h), flag, seq);
+    RS_HIP(hipGetLastError());
+    if (!(fl && pc_poll_flags(h, nb, seq))) RS_HIP(hipStreamSynchronize(h->stream));
+    return RS_OK;
+}
+
 int rs_pc_read(rs_pc* h, double* host) {
     rs::clear_error();
     RS_CHECK(h && host, RS_ERR_ARG, "null argument");
@@ -4295,27 +4354,22 @@ int rs_pc_read(rs_pc* h, double* host) {
         RS_HIP(hipHostMalloc(&h->hRead, sizeof(double) * h->n, hipHostMallocMapped | hipHostMallocCoherent));
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hReadDev), h->hRead, 0));
     }
-    if (!dma) {
-        bool done = false;
-        RS_TRY(pc_halo_settle_read(h, h->hReadDev, &done));
-        if (done) {
-            std::memcpy(host, h->hRead, sizeof(double) * h->n);
-            return RS_OK;
-        }
+    if (dma) {
+        RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
+        const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
+        if (h->prec == RS_PREC_F32)
+            hipLaunchKernelGGL((pc_export_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
+                               static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)pc_thfast(h));
+        else
+            hipLaunchKernelGGL((pc_export_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
+                               static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)pc_thfast(h));
+        RS_HIP(hipGetLastError());
+        RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+        RS_HIP(hipStreamSynchronize(h->stream));
+        return RS_OK;
     }
-    RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
-    double* dst = dma ? h->dTmp : h->hReadDev;
-    const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
-    if (h->prec == RS_PREC_F32)
-        hipLaunchKernelGGL((pc_export_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
-    else
-        hipLaunchKernelGGL((pc_export_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
-    RS_HIP(hipGetLastError());
-    if (dma) RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
-    RS_HIP(hipStreamSynchronize(h->stream));
-    if (!dma) std::memcpy(host, h->hRead, sizeof(double) * h->n);
+    RS_TRY(pc_read_volume(h, h->hReadDev));
+    std::memcpy(host, h->hRead, sizeof(double) * h->n);
     return RS_OK;
 }
 
@@ -4326,19 +4380,7 @@ int rs_pc_read_pinned(rs_pc* h, double* pinned) {
     RS_HIP(hipSetDevice(h->device));
     double* dst = nullptr;
     RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), pinned, 0));
-    bool done = false;
-    RS_TRY(pc_halo_settle_read(h, dst, &done));   // (halo: a pending state, settled as it is read)
-    if (done) return RS_OK;
-    const int nb = (int)std::min<size_t>(1024, (h->n / 2 + NT - 1) / NT + 1);
-    if (h->prec == RS_PREC_F32)
-        hipLaunchKernelGGL((pc_export2_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
-    else
-        hipLaunchKernelGGL((pc_export2_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                           static_cast<const double*>(h->dP), dst, h->X, h->Y, h->TH, (int)pc_thfast(h));
-    RS_HIP(hipGetLastError());
-    RS_HIP(hipStreamSynchronize(h->stream));
-    return RS_OK;
+    return pc_read_volume(h, dst);
 }
 
 int rs_pc_write(rs_pc* h, const double* host) {

@@ -1,6 +1,8 @@
 """Pose-cell network on the GPU vs the reference (golden trajectories) and the
 oracle.  Tolerance (BASELINE.json north_star): float32 activations within 1e-5
 of the float64 reference, argmax identical; float64 path within 1e-12."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -489,6 +491,34 @@ def test_eager_readback_equals_lazy(pcn):
     assert np.array_equal(a.posecells, b.posecells)  # run() invalidated the export
     with pytest.raises(ValueError):
         pcn(shape, readback='sometimes')
+
+
+@pytest.mark.parametrize('shape,precision', [((21, 21, 35), 'float32'), ((21, 21, 35), 'float64'),
+                                             ((50, 50, 10), 'float32'), ((128, 128, 72), 'float32')])
+def test_volume_reads_vs_c_oracle(pcn, shape, precision):
+    """Every way the volume reaches the host -- the pinned read (`.posecells`), the
+    copying rs_pc_read and the eager readback -- against the C oracle, on an odd-sized
+    volume (the export's lone last cell), the simulate grid and the column form's
+    128x128x72 (a capped export grid: several 16-byte pieces per thread).  The export
+    kernel's blocks' flags are polled by the host (pc_read_volume)."""
+    from oracle import c_oracle as C
+    from pyratslam_amd import _lib
+    tol = F32_TOL if precision == 'float32' else F64_TOL
+    a, b = pcn(shape, precision=precision), pcn(shape, precision=precision, readback='eager')
+    ref = C.PoseCellC(shape)
+    loc = tuple(x // 2 for x in shape)
+    for n in (a, b, ref):
+        n.inject(1, loc)
+    buf = np.empty(shape)
+    for v in odometry(4, 31):
+        want = ref.update(v)
+        assert a.update(v) == want and b.update(v) == want
+        assert np.abs(b.posecells - ref.posecells).max() < tol
+        assert np.abs(a.posecells - ref.posecells).max() < tol
+        _lib.check(a._lib.rs_pc_read(a._h, _lib.ptr(buf, ctypes.c_double)))
+        assert np.array_equal(buf, a.posecells)
+    a.close()
+    b.close()
 
 
 @pytest.mark.parametrize('precision,tol', [('float32', F32_TOL), ('float64', F64_TOL)])
