@@ -272,8 +272,10 @@ int rs_vt_resolve(rs_vt* h, int nq, const uint64_t* global_keys, int mode, uint6
  * rs_vt_match_stream over HBM-resident batches, its one scan of all batches;
  * -1 when that scan ran untimed or the call ran several scans */
 int rs_vt_last_ms(rs_vt* h, double* ms);
-/* HIP events around every scan (default on); off drops two stream markers per
- * match call (a ~5 us gap between the scan and the result export) */
+/* HIP events around every scan (default off).  Off, a match call's keys are polled in
+ * pinned host memory (a plane scan's last block exports them itself) instead of a
+ * stream synchronisation; on, two stream markers bracket each scan and the call
+ * synchronises (rs_vt_last_ms) */
 int rs_vt_set_timing(rs_vt* h, int enable);
 /* which scan kernel family the handle uses for its shape: "plane" (bit-plane
  * borrow count, W == 32, H in {32, 64}, max_offset 8), "carry" (byte-SWAR carry

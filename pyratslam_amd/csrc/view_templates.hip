@@ -127,6 +127,10 @@ struct ScanOut {
     unsigned long long* best;  // [nq] packed keys (MATRIX == false)
     uint32_t* mat;             // [nq][ld]          (MATRIX == true)
     int64_t ld;
+    // plane scan, MATRIX == false: the block that finishes last hands the keys to the
+    // host words and resets them (vt_keys_export folded in); done counts the blocks
+    unsigned long long* host = nullptr;
+    unsigned* done = nullptr;
 };
 
 template <bool MATRIX>
@@ -448,7 +452,8 @@ __device__ inline void transpose4x4_bytes(uint32_t a, uint32_t b, uint32_t c, ui
 // stores.  Bit b of plane k = bit k of pixel (row + b/8, col 8cg + b%8).
 __global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restrict__ raw, int H,
                                                         int M, uint32_t* __restrict__ qp,
-                                                        uint32_t* __restrict__ qsum) {
+                                                        uint32_t* __restrict__ qsum,
+                                                        uint8_t* __restrict__ raw_copy) {
     constexpr int W = 8 * PL_CG;
     __shared__ uint32_t s_red[4];
     __shared__ uint2 s_t[64 * W / 8];   // transposed segments (H <= 64)
@@ -459,6 +464,8 @@ __global__ __launch_bounds__(256) void vt_qplane_kernel(const uint8_t* __restric
     uint32_t part = 0;
     for (int d = threadIdx.x; d < H * W / 8; d += blockDim.x) {
         uint2 v = reinterpret_cast<const uint2*>(Q)[d];
+        // raw read in place from pinned host memory: its bytes also into the device copy
+        if (raw_copy) reinterpret_cast<uint2*>(raw_copy + (size_t)blockIdx.x * H * W)[d] = v;
         const int r = d / (W / 8);
         const bool live = r >= M && r < H - M;
         if (live) part = __builtin_amdgcn_sad_u8(v.y, 0u, __builtin_amdgcn_sad_u8(v.x, 0u, part));
@@ -777,6 +784,32 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
     // counter's last user in this launch: it rewinds the counter for the next launch
     // (no memset).
     if (threadIdx.x == 0 && failed == (unsigned)(nbatch + nqc / G - 1)) *ctr = 0u;
+    if constexpr (!MATRIX) {
+        if (out.host) {   // (kernel argument: uniform)
+            // The key export folded into the scan (small calls, vt_scan_local_impl): the
+            // keys are agent-scope atomics (performed at memory, never held in an L2), each
+            // wave waits for its own (vmcnt(0)) before the block's counter add, the last
+            // adder learns it from the add's return value and reads the keys with sc1
+            // loads only -- the hand-off pc_halo_finish uses (MI355X_MICROARCH.md's
+            // hand-off rows), then stores them into the pinned host words and resets them.
+            __shared__ int s_last;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                s_last = __hip_atomic_fetch_add(out.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                         gridDim.x - 1;
+            __syncthreads();
+            if (s_last) {
+                for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+                    const unsigned long long k =
+                        __hip_atomic_load(out.best + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(out.best + i, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(out.host + i, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                if (threadIdx.x == 0) __hip_atomic_store(out.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
     VT_STAMP(1);
 }
 
@@ -894,7 +927,11 @@ struct rs_vt {
     // query staging
     int qCap = 0;
     uint8_t* dQraw = nullptr;
-    uint8_t* hQraw = nullptr;  // pinned
+    uint8_t* hQraw = nullptr;  // pinned, fine-grained (a small batch's plane kernel reads it in place)
+    uint8_t* hQrawDev = nullptr;  // hQraw in the device's address space
+    bool qrawBusy = false;     // hQraw read by queued work not yet known to have run
+    hipEvent_t evQraw = nullptr;  // recorded after that work when the call returns without waiting
+    bool qrawEvRecorded = false;
     uint2* dQf = nullptr;
     uint32_t* dQsum = nullptr;
     unsigned long long* dBest = nullptr;
@@ -930,7 +967,7 @@ struct rs_vt {
     uint32_t* dMat = nullptr;
     uint32_t* hMat = nullptr;  // pinned
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool timing = true;  // HIP events around every scan (rs_vt_set_timing)
+    bool timing = false;  // HIP events around every scan (rs_vt_set_timing; off: the keys are polled)
     bool timedScan = false;  // the last scan recorded ev0/ev1
     float lastMs = 0.f;
     int stagedQ = 0;  // queries staged by the last scan
@@ -945,6 +982,8 @@ struct rs_vt {
     uint32_t* dQsumRaw = nullptr;
     int planeSlots = 0;  // resident plane-scan blocks on the device (occupancy x CUs)
     unsigned* dCtr = nullptr;  // per template block x query group: next batch (plane scan)
+    unsigned* dDone = nullptr; // plane scan blocks finished (the folded key export; reset by the last)
+    bool keysFolded = false;   // the running scan exports its own keys (vt_fetch_keys: no export launch)
     int ctrCap = 0;
     // on-device subsampling of camera frames (rs_vt_set_subsample / rs_vt_match_frames)
     int32_t* dPix = nullptr;   // H*W byte offsets of the kept pixels in a frame
@@ -1017,12 +1056,29 @@ int vt_grow_lib(rs_vt* h, int64_t need_slots) {
     return RS_OK;
 }
 
+// hQraw (pinned) is read by queued copies and, for small batches, in place by the plane
+// kernel: before the host writes or frees it again that work must have run.  A call that
+// returns without waiting for its work (rs_vt_add) records evQraw after it; a call that
+// waits for its keys (vt_fetch_keys) clears the flag; otherwise (an error between the
+// staging and the wait) the stream is synchronised.
+int vt_qraw_idle(rs_vt* h) {
+    if (h->qrawBusy) {
+        if (h->qrawEvRecorded) RS_HIP(hipEventSynchronize(h->evQraw));
+        else RS_HIP(hipStreamSynchronize(h->stream));
+        h->qrawBusy = false;
+        h->qrawEvRecorded = false;
+    }
+    return RS_OK;
+}
+
 int vt_grow_queries(rs_vt* h, int nq) {
     if (nq <= h->qCap) return RS_OK;
     int cap = h->qCap > 0 ? h->qCap : 64;
     while (cap < nq) cap *= 2;
     if (h->dQraw) RS_HIP(hipFree(h->dQraw));
+    RS_TRY(vt_qraw_idle(h));
     if (h->hQraw) RS_HIP(hipHostFree(h->hQraw));
+    h->hQraw = h->hQrawDev = nullptr;
     if (h->dQf) RS_HIP(hipFree(h->dQf));
     if (h->dQsum) RS_HIP(hipFree(h->dQsum));
     if (h->dBest) RS_HIP(hipFree(h->dBest));
@@ -1036,7 +1092,8 @@ int vt_grow_queries(rs_vt* h, int nq) {
         RS_HIP(hipMalloc(&h->dQsumRaw, sizeof(uint32_t) * cap));
     }
     RS_HIP(hipMalloc(&h->dQraw, qb * cap));
-    RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocDefault));
+    RS_HIP(hipHostMalloc(&h->hQraw, qb * cap, hipHostMallocMapped | hipHostMallocCoherent));
+    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hQrawDev), h->hQraw, 0));
     RS_HIP(hipMalloc(&h->dQf, sizeof(uint2) * (size_t)h->WD * h->H * cap));
     RS_HIP(hipMalloc(&h->dQsum, sizeof(uint32_t) * cap));
     RS_HIP(hipMalloc(&h->dBest, sizeof(unsigned long long) * cap));
@@ -1092,11 +1149,32 @@ int vt_grow_cand(rs_vt* h, int64_t slots) {
 
 int vt_build_forms(rs_vt* h, int nq);
 
+// Batches of at most this many queries are read by the plane kernel straight from the
+// pinned staging array (one launch in place of a host-to-device copy and the launch;
+// the kernel leaves the raw bytes in dQraw for the template stores); RS_VT_ZC=0: always
+// the copy.
+constexpr int VT_ZC_MAX = 64;
+bool vt_zc_env() {
+    static const bool on = [] {
+        const char* e = std::getenv("RS_VT_ZC");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
 // Upload nq raw queries and build their forms on the device.
 int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     RS_TRY(vt_grow_queries(h, nq));
+    RS_TRY(vt_qraw_idle(h));
     const size_t qb = (size_t)h->H * h->W * nq;
     std::memcpy(h->hQraw, queries, qb);
+    h->qrawBusy = true;
+    if (h->planar && nq <= VT_ZC_MAX && vt_zc_env()) {
+        hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, h->hQrawDev, h->H, h->M, h->dQp,
+                           h->dQsumRaw, h->dQraw);
+        RS_HIP(hipGetLastError());
+        return RS_OK;
+    }
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
     return vt_build_forms(h, nq);
 }
@@ -1109,7 +1187,7 @@ int vt_build_forms(rs_vt* h, int nq, const uint8_t* src) {
                            h->WD, h->M, h->dQf, h->dQsum);
     else
         hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, src, h->H,
-                           h->M, h->dQp, h->dQsumRaw);
+                           h->M, h->dQp, h->dQsumRaw, nullptr);
     RS_HIP(hipGetLastError());
     return RS_OK;
 }
@@ -1318,7 +1396,7 @@ int vt_append_staged(rs_vt* h, const std::vector<std::pair<int, int64_t>>& news)
 
 // Stage nq queries (raw H x W, or whole frames subsampled on the device) and
 // min-reduce their local first-argmin keys into dBest.
-int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = false) {
+int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = false, bool fold_ok = true) {
     RS_CHECK(h, RS_ERR_STATE, "null view-template handle");
     RS_CHECK(nq >= 0, RS_ERR_ARG, "negative query count");
     if (nq == 0) return RS_OK;
@@ -1341,6 +1419,18 @@ int vt_scan_local_impl(rs_vt* h, int nq, const uint8_t* queries, bool frames = f
     h->bestClean = 0;
     const int64_t lc = local_count_of(h, h->count);
     ScanOut out{h->dBest, nullptr, 0};
+    // a plane scan whose keys the host polls exports them itself (its last block): one
+    // launch fewer per call.  Not when they are min-reduced over ranks first.
+    h->keysFolded = fold_ok && h->planar && lc > 0 && vt_poll_env() && !h->timing && nq <= VT_POLL_MAX;
+    if (h->keysFolded) {
+        if (!h->dDone) {
+            RS_HIP(hipMalloc(&h->dDone, sizeof(unsigned)));
+            RS_HIP(hipMemsetAsync(h->dDone, 0, sizeof(unsigned), h->stream));
+        }
+        for (int i = 0; i < nq; ++i) h->hBest[i] = KEY_PENDING;
+        out.host = h->hBestDev;
+        out.done = h->dDone;
+    }
     if (h->timing) RS_HIP(hipEventRecord(h->ev0, h->stream));
     RS_TRY(vt_launch_scan<false>(h, false, lc, nq, out, h->rank, h->nranks));
     if (h->timing) RS_HIP(hipEventRecord(h->ev1, h->stream));
@@ -1432,15 +1522,23 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
                  ncclGetErrorString(r));
     }
     const bool poll = vt_poll_env() && !h->timedScan && nq <= VT_POLL_MAX;
-    if (poll)
-        for (int i = 0; i < nq; ++i) h->hBest[i] = KEY_PENDING;
-    hipLaunchKernelGGL(vt_keys_export, dim3((nq + 255) / 256 < 64 ? (nq + 255) / 256 : 64), dim3(256), 0,
-                       h->stream, h->dBest, nq, h->hBestDev);
-    RS_HIP(hipGetLastError());
+    if (h->keysFolded) {   // the scan's last block exports them (vt_scan_local_impl)
+        h->keysFolded = false;
+    } else {
+        if (poll)
+            for (int i = 0; i < nq; ++i) h->hBest[i] = KEY_PENDING;
+        hipLaunchKernelGGL(vt_keys_export, dim3((nq + 255) / 256 < 64 ? (nq + 255) / 256 : 64), dim3(256), 0,
+                           h->stream, h->dBest, nq, h->hBestDev);
+        RS_HIP(hipGetLastError());
+    }
     if (!(poll && vt_poll_keys(h->hBest, nq))) {
         RS_HIP(hipStreamSynchronize(h->stream));
         h->stagingBusy = false;
     }
+    // the keys are the call's last work: everything queued before them has run,
+    // the readers of hQraw included (not the staging copies vt_store queues after them)
+    h->qrawBusy = false;
+    h->qrawEvRecorded = false;
     h->bestClean = h->bestPending;
     if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     return RS_OK;
@@ -1633,7 +1731,7 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
 int vt_match_impl(rs_vt* h, int nq, const uint8_t* queries, int mode, uint64_t* best_score,
                   int64_t* best_index, uint8_t* is_new, bool frames = false) {
     RS_CHECK(mode == RS_VT_FROZEN || mode == RS_VT_SEQUENTIAL, RS_ERR_ARG, "unknown mode %d", mode);
-    RS_TRY(vt_scan_local_impl(h, nq, queries, frames));
+    RS_TRY(vt_scan_local_impl(h, nq, queries, frames, h->nranks == 1));
     if (nq == 0) return RS_OK;
     RS_TRY(vt_fetch_keys(h, nq, true));
     return vt_resolve_impl(h, nq, h->hBest, mode, best_score, best_index, is_new);
@@ -1726,7 +1824,7 @@ int rs_vt_destroy(rs_vt* h) {
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
                     (void*)h->dLibTs, (void*)h->dCandP, (void*)h->dCandTs, (void*)h->dQp,
-                    (void*)h->dQsumRaw, (void*)h->dCtr, (void*)h->dPix, (void*)h->dFrames})
+                    (void*)h->dQsumRaw, (void*)h->dCtr, (void*)h->dDone, (void*)h->dPix, (void*)h->dFrames})
         if (p) (void)hipFree(p);
     if (h->hStream) (void)hipHostFree(h->hStream);
     if (h->dStream) (void)hipFree(h->dStream);
@@ -1739,6 +1837,7 @@ int rs_vt_destroy(rs_vt* h) {
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evScan) (void)hipEventDestroy(h->evScan);
     if (h->evComm) (void)hipEventDestroy(h->evComm);
+    if (h->evQraw) (void)hipEventDestroy(h->evQraw);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
     for (int i = 0; i < 2; ++i) {
         if (h->dUp[i]) (void)hipFree(h->dUp[i]);
@@ -1765,14 +1864,20 @@ int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
     if (first_index) *first_index = h->count;
     if (n == 0) return RS_OK;
     RS_TRY(vt_grow_queries(h, n));
+    RS_TRY(vt_qraw_idle(h));
     const size_t qb = (size_t)h->H * h->W * n;
     std::memcpy(h->hQraw, templates, qb);
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    h->qrawBusy = true;
     h->stagedQ = 0;  // the staging buffer now holds templates, not a query batch
     std::vector<std::pair<int, int64_t>> news;
     news.reserve(n);
     for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
     RS_TRY(vt_append_staged(h, news));   // (its copies guarded by vt_staging_idle, not a sync)
+    // the call returns with the copy from hQraw queued: the next write of hQraw waits for it
+    if (!h->evQraw) RS_HIP(hipEventCreateWithFlags(&h->evQraw, hipEventDisableTiming));
+    RS_HIP(hipEventRecord(h->evQraw, h->stream));
+    h->qrawEvRecorded = true;
     return RS_OK;
 }
 

@@ -158,6 +158,48 @@ def test_sequential_batch_equals_oracle_sequence(vtmod):
     assert np.array_equal(np.stack([t.template for t in lib.templates]), np.stack(ref.templates))
 
 
+def test_small_batches_in_place_and_back_to_back_adds(vtmod):
+    """Batches of at most 64 queries are read by the plane kernel straight from the
+    pinned staging array (which also leaves their bytes on the device for the template
+    stores); larger ones are copied first.  Templates added in small chunks back to back
+    (each rs_vt_add returns with its copy from the staging array queued; the next one
+    waits for it before overwriting the array), then single queries, 64 and 65 queries
+    against the oracle, every pair score of the device library, and single-query
+    sequential matching (a query that becomes a template is stored from the device copy
+    the plane kernel made) against the reference's match sequence."""
+    lib_np = V.synthetic_library(200, 64, 32, seed=21)
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    i, k = 0, 0
+    while i < len(lib_np):
+        n = 1 + k % 4
+        lib.add(lib_np[i:i + n])
+        i += n
+        k += 1
+    queries, _ = V.synthetic_queries(lib_np, 150, seed=22)
+    ref = np.stack([V.vt_scores_library(lib_np, q) for q in queries])
+    for j in range(12):
+        idx, score, _ = lib.match_templates(queries[j:j + 1], mode=0)
+        assert idx[0] == ref[j].argmin() and score[0] == ref[j].min(), j
+    for a, b in ((12, 76), (76, 141)):           # 64 queries in place, 65 copied
+        idx, score, _ = lib.match_templates(queries[a:b], mode=0)
+        assert np.array_equal(idx, ref[a:b].argmin(axis=1)) and np.array_equal(score, ref[a:b].min(axis=1))
+    assert np.array_equal(lib.scores(queries[:9]), ref[:9])
+    base = V.synthetic_library(30, 64, 32, seed=23)
+    rng = np.random.default_rng(24)
+    qs = np.array([np.clip(np.roll(base[int(rng.integers(0, 30))], int(rng.integers(-6, 7)), axis=0).astype(int)
+                           - rng.integers(0, 3 if rng.random() < 0.7 else 60, (64, 32)), 0, 255)
+                   for _ in range(120)], dtype=np.uint8)
+    oracle = V.ViewTemplatesOracle((0, 128), (0, 64), 2, 2, 8, 8, 45000)
+    oracle.shape = (64, 32)
+    expect = [oracle.match_template(q)[0] for q in qs]
+    seq = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    got = [int(seq.match_templates(q[None])[0][0]) for q in qs]
+    assert got == expect
+    assert np.array_equal(np.stack([t.template for t in seq.templates]), np.stack(oracle.templates))
+    assert np.array_equal(seq.scores(qs[:5]), np.stack([V.vt_scores_library(np.stack(oracle.templates), q)
+                                                         for q in qs[:5]]))
+
+
 def test_ties_pick_first_index(vtmod):
     t = V.synthetic_library(5, 64, 32, seed=2)
     lib_np = np.concatenate([t, t, t])                       # indices 0..4 repeated
