@@ -52,6 +52,42 @@ def kernel_3d(dim_e=PC_E_DIM, dim_i=PC_I_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_S
     return k
 
 
+def diff_gaussian(dim_e=PC_E_DIM, dim_i=PC_I_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA, order=3):
+    """diff_gaussian(order=1, 2 or 3) (posecell_network.py:97-142): a DoG over a cube,
+    square or line of max(dim_e, dim_i) taps with the reference's window masks and
+    per-order coefficients -- 1/(s*sqrt(2pi))^3, 1/(s*s*2*pi), 1/(s*sqrt(2pi)) -- each
+    tap one scalar ``math.exp`` per Gaussian, then divided by |sum| (numpy's sum).
+    Order 3 is ``kernel_3d`` (the network's excitation kernel); the reference keeps
+    orders 2 and 1 as attributes it never uses (:30-31).  Other orders return None,
+    as the reference's fall-through does."""
+    if order == 3:
+        return kernel_3d(dim_e, dim_i, sigma_e, sigma_i)
+    if order not in (1, 2):
+        return None
+    dim = max(dim_e, dim_i)
+    c = dim // 2
+    if order == 2:
+        ce, ci = 1.0 / (sigma_e * sigma_e * 2 * math.pi), 1.0 / (sigma_i * sigma_i * 2 * math.pi)
+    else:
+        ce, ci = _gauss_coef(sigma_e, 1), _gauss_coef(sigma_i, 1)
+    f = np.empty((dim,) * order)
+    for idx in np.ndindex(*f.shape):
+        hi, lo = max(idx), min(idx)
+        r = sum((v - c) ** 2 for v in idx)
+        me = 1 if hi <= c + dim_e and lo >= c - dim_e else 0
+        mi = 1 if hi <= c + dim_i and lo >= c - dim_i else 0
+        f[idx] = me * ce * math.exp(-r / (2 * sigma_e ** 2)) - mi * ci * math.exp(-r / (2 * sigma_i ** 2))
+    f /= abs(np.sum(f.ravel()))
+    return f
+
+
+def diff_gaussian_separable(dim_e=PC_E_DIM, dim_i=PC_I_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA):
+    """diff_gaussian_separable (posecell_network.py:192-208): the order-1 DoG, cube
+    rooted (the reference's own FIXME: a DoG is not separable; kept as the attribute
+    ``kernel_1d_sep``, unused)."""
+    return cbrt(diff_gaussian(dim_e, dim_i, sigma_e, sigma_i, order=1))
+
+
 def separable_factors(dim=PC_E_DIM, sigma_e=PC_E_SIGMA, sigma_i=PC_I_SIGMA):
     """(ge, gi, scale) with kernel_3d == (ge x ge x ge - gi x gi x gi) * scale.
 

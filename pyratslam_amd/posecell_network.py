@@ -123,6 +123,10 @@ class PoseCellNetwork:
         self.pc_vtrans_scale = PC_CELL_X_SIZE
         self.pc_vrot_scale = 2.0 * np.pi / self.shape[2]
         self.kernel_3d = F.kernel_3d()
+        # the reference's unused attributes (posecell_network.py:30-32)
+        self.kernel_2d = F.diff_gaussian(order=2)
+        self.kernel_1d = F.diff_gaussian(order=1)
+        self.kernel_1d_sep = F.diff_gaussian_separable()
         self.filter_table = F.FilterTable()
         self.filter_dict_2d = self.filter_table.dict
         self.filter_dict_2d_precision = F.LUT_PRECISION
@@ -384,6 +388,12 @@ class PoseCellNetwork:
         return float(ms[0]), float(ms[1])
 
     # -- filter helpers of the reference class (host-side, NumPy) -----------------
+    def diff_gaussian(self, dim_e, dim_i, sigma_e, sigma_i, order=3):
+        return F.diff_gaussian(dim_e, dim_i, sigma_e, sigma_i, order)
+
+    def diff_gaussian_separable(self, dim_e, dim_i, sigma_e, sigma_i):
+        return F.diff_gaussian_separable(dim_e, dim_i, sigma_e, sigma_i)
+
     def diff_gaussian_offset_2d(self, sigma_e, sigma_i, shape=(7, 7), origin=(0, 0)):
         return F.filter_2d(origin, sigma_e, sigma_i, shape)
 

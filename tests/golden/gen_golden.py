@@ -252,6 +252,9 @@ def gen_kernels(pn, out):
     np.savez_compressed(
         os.path.join(out, 'kernels.npz'),
         kernel_3d=net.kernel_3d,
+        kernel_2d=net.kernel_2d,
+        kernel_1d=net.kernel_1d,
+        kernel_1d_sep=net.kernel_1d_sep,
         lut_keys=np.array(keys, dtype=np.int64),
         lut_filters=np.stack([lut[k] for k in keys]),
         f1d_origins=np.arange(-4, 5),

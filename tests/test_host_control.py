@@ -16,6 +16,19 @@ def test_kernel_3d_matches_reference_bits():
     assert np.array_equal(F.kernel_3d(), load_golden('kernels')['kernel_3d'])
 
 
+def test_unused_reference_kernels_match_reference_bits():
+    """kernel_2d, kernel_1d and kernel_1d_sep (posecell_network.py:30-32), kept by the
+    reference as attributes it never uses: bit-identical to the reference-made golden
+    values (diff_gaussian orders 2 and 1, diff_gaussian_separable); order 3 is kernel_3d,
+    any other order None, as the reference's fall-through."""
+    g = load_golden('kernels')
+    assert np.array_equal(F.diff_gaussian(order=2), g['kernel_2d'])
+    assert np.array_equal(F.diff_gaussian(order=1), g['kernel_1d'])
+    assert np.array_equal(F.diff_gaussian_separable(), g['kernel_1d_sep'])
+    assert np.array_equal(F.diff_gaussian(order=3), g['kernel_3d'])
+    assert F.diff_gaussian(order=4) is None
+
+
 def test_separable_factors_reconstruct_kernel():
     ge, gi, scale = F.separable_factors()
     k = (np.einsum('i,j,k->ijk', ge, ge, ge) - np.einsum('i,j,k->ijk', gi, gi, gi)) * scale

@@ -83,6 +83,26 @@ def test_network_death_vs_reference(pcn, monkeypatch, name, form, precision, tol
     assert np.abs(b.posecells - dense_state(case, len(odom) - 1)).max() < tol
 
 
+def test_reference_attributes(pcn):
+    """The reference's public attributes (posecell_network.py:24-48): shape, the zero
+    state, the four kernels (three of them unused by the reference too), the scales,
+    the 2-D filter LUT and its key precision, bit-identical to the reference-made golden
+    values."""
+    g = load_golden('kernels')
+    net = pcn((21, 21, 36))
+    assert net.shape == (21, 21, 36) and (net.posecells == 0).all() and net.max_pc is None
+    for name in ('kernel_3d', 'kernel_2d', 'kernel_1d', 'kernel_1d_sep'):
+        assert np.array_equal(getattr(net, name), g[name]), name
+    assert np.array_equal(net.diff_gaussian(7, 5, 1, 2, order=2), g['kernel_2d'])
+    assert np.array_equal(net.diff_gaussian_separable(7, 5, 1, 2), g['kernel_1d_sep'])
+    assert net.global_inhibition == 0.2 and net.pc_vtrans_scale == 0.2
+    assert net.pc_vrot_scale == 2.0 * np.pi / 36 and net.filter_dict_2d_precision == 10
+    keys = [tuple(k) for k in g['lut_keys']]
+    assert sorted(net.filter_dict_2d.keys()) == keys
+    assert all(np.array_equal(net.filter_dict_2d[k], f) for k, f in zip(keys, g['lut_filters']))
+    net.close()
+
+
 def test_run_equals_repeated_update(pcn):
     # 4,200 steps in one run(): more results than one pass of the export kernel's
     # grid (64 blocks x 64 steps), so its grid-stride loop is exercised
