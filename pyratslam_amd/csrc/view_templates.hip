@@ -1075,8 +1075,8 @@ int vt_grow_queries(rs_vt* h, int nq) {
     if (nq <= h->qCap) return RS_OK;
     int cap = h->qCap > 0 ? h->qCap : 64;
     while (cap < nq) cap *= 2;
-    if (h->dQraw) RS_HIP(hipFree(h->dQraw));
     RS_TRY(vt_qraw_idle(h));
+    if (h->dQraw) RS_HIP(hipFree(h->dQraw));
     if (h->hQraw) RS_HIP(hipHostFree(h->hQraw));
     h->hQraw = h->hQrawDev = nullptr;
     if (h->dQf) RS_HIP(hipFree(h->dQf));
