@@ -298,6 +298,8 @@ class ViewTemplates:
     def match_batch(self, images, pcs):
         """``[match(im, *pc) for im, pc in zip(images, pcs)]`` in one call."""
         q = [self.subsample(im) for im in images]
+        if not q:
+            return []
         if self._float or any(x.dtype != np.uint8 for x in q):
             return [self._match_float(x, pc) for x, pc in zip(q, pcs)]
         idx, _, _ = self.match_templates(np.stack(q), pcs)

@@ -200,6 +200,38 @@ def test_small_batches_in_place_and_back_to_back_adds(vtmod):
                                                          for q in qs[:5]]))
 
 
+def test_zero_sized_calls(vtmod):
+    """Empty inputs at every entry point return empty results and leave the library as
+    it was: no queries (match_templates, match_batch, match_stream with nb = 0 or
+    nq = 0, host and HBM-resident), no templates added, scores against an empty
+    library, and an ordinary match afterwards."""
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(70, 64, 32, seed=31)
+    lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+    assert lib.scores(lib_np[:2]).shape == (2, 0)
+    lib.add(lib_np[:0])
+    assert lib.count() == 0
+    lib.add(lib_np)
+    idx, score, new = lib.match_templates(np.empty((0, 64, 32), np.uint8), mode=0)
+    assert idx.shape == score.shape == new.shape == (0,)
+    idx, score, new = lib.match_templates(np.empty((0, 64, 32), np.uint8))
+    assert idx.shape == (0,) and lib.count() == 70
+    for shape in ((0, 5, 64, 32), (3, 0, 64, 32)):
+        i, sc = lib.match_stream(np.empty(shape, np.uint8))
+        assert i.shape == sc.shape == shape[:2]
+    buf = _lib.DeviceBuffer(64 * 32 * 4)
+    i, sc = lib.match_stream((0, 4, buf))
+    assert i.shape == (0, 4)
+    buf.close()
+    q, src = V.synthetic_queries(lib_np, 5, seed=32)
+    ref = np.stack([V.vt_scores_library(lib_np, x) for x in q])
+    idx, score, _ = lib.match_templates(q, mode=0)
+    assert np.array_equal(idx, ref.argmin(axis=1)) and np.array_equal(score, ref.min(axis=1))
+    assert lib.count() == 70
+    ros = vtmod.ViewTemplates((32, 96), (32, 96), 2, 2, 256, 256, 45000)
+    assert ros.match_batch([], []) == [] and len(ros.templates) == 0
+
+
 def test_ties_pick_first_index(vtmod):
     t = V.synthetic_library(5, 64, 32, seed=2)
     lib_np = np.concatenate([t, t, t])                       # indices 0..4 repeated
