@@ -930,8 +930,6 @@ struct rs_vt {
     uint8_t* hQraw = nullptr;  // pinned, fine-grained (a small batch's plane kernel reads it in place)
     uint8_t* hQrawDev = nullptr;  // hQraw in the device's address space
     bool qrawBusy = false;     // hQraw read by queued work not yet known to have run
-    hipEvent_t evQraw = nullptr;  // recorded after that work when the call returns without waiting
-    bool qrawEvRecorded = false;
     uint2* dQf = nullptr;
     uint32_t* dQsum = nullptr;
     unsigned long long* dBest = nullptr;
@@ -1056,17 +1054,15 @@ int vt_grow_lib(rs_vt* h, int64_t need_slots) {
     return RS_OK;
 }
 
-// hQraw (pinned) is read by queued copies and, for small batches, in place by the plane
-// kernel: before the host writes or frees it again that work must have run.  A call that
-// returns without waiting for its work (rs_vt_add) records evQraw after it; a call that
-// waits for its keys (vt_fetch_keys) clears the flag; otherwise (an error between the
-// staging and the wait) the stream is synchronised.
+// hQraw (pinned) is read by a queued copy (RS_VT_STAGE=pinned) or, for small batches, in
+// place by the plane kernel: before the host writes or frees it again that work must
+// have run.  Every call that stages into it waits for its keys before returning
+// (vt_fetch_keys clears the flag); after an error between the staging and that wait the
+// stream is synchronised here.  (rs_vt_add uploads the caller's array directly.)
 int vt_qraw_idle(rs_vt* h) {
     if (h->qrawBusy) {
-        if (h->qrawEvRecorded) RS_HIP(hipEventSynchronize(h->evQraw));
-        else RS_HIP(hipStreamSynchronize(h->stream));
+        RS_HIP(hipStreamSynchronize(h->stream));
         h->qrawBusy = false;
-        h->qrawEvRecorded = false;
     }
     return RS_OK;
 }
@@ -1167,14 +1163,28 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     RS_TRY(vt_grow_queries(h, nq));
     RS_TRY(vt_qraw_idle(h));
     const size_t qb = (size_t)h->H * h->W * nq;
-    std::memcpy(h->hQraw, queries, qb);
-    h->qrawBusy = true;
+    // larger batches: HIP's own upload of the caller's (pageable) array, which returns
+    // once the bytes are staged (per-batch PCIe-inclusive rate 4.04-4.12 against 3.44-3.54
+    // G compares/s through our memcpy into pinned staging, round 5); RS_VT_STAGE=pinned:
+    // the memcpy
+    static const bool direct = [] {
+        const char* e = std::getenv("RS_VT_STAGE");
+        return !(e && std::strcmp(e, "pinned") == 0);
+    }();
     if (h->planar && nq <= VT_ZC_MAX && vt_zc_env()) {
+        std::memcpy(h->hQraw, queries, qb);
+        h->qrawBusy = true;
         hipLaunchKernelGGL(vt_qplane_kernel, dim3(nq), dim3(256), 0, h->stream, h->hQrawDev, h->H, h->M, h->dQp,
                            h->dQsumRaw, h->dQraw);
         RS_HIP(hipGetLastError());
         return RS_OK;
     }
+    if (direct) {
+        RS_HIP(hipMemcpyAsync(h->dQraw, queries, qb, hipMemcpyHostToDevice, h->stream));
+        return vt_build_forms(h, nq);
+    }
+    std::memcpy(h->hQraw, queries, qb);
+    h->qrawBusy = true;
     RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
     return vt_build_forms(h, nq);
 }
@@ -1538,7 +1548,6 @@ int vt_fetch_keys(rs_vt* h, int nq, bool allreduce) {
     // the keys are the call's last work: everything queued before them has run,
     // the readers of hQraw included (not the staging copies vt_store queues after them)
     h->qrawBusy = false;
-    h->qrawEvRecorded = false;
     h->bestClean = h->bestPending;
     if (h->timedScan) RS_HIP(hipEventElapsedTime(&h->lastMs, h->ev0, h->ev1));
     return RS_OK;
@@ -1837,7 +1846,6 @@ int rs_vt_destroy(rs_vt* h) {
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->evScan) (void)hipEventDestroy(h->evScan);
     if (h->evComm) (void)hipEventDestroy(h->evComm);
-    if (h->evQraw) (void)hipEventDestroy(h->evQraw);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
     for (int i = 0; i < 2; ++i) {
         if (h->dUp[i]) (void)hipFree(h->dUp[i]);
@@ -1864,20 +1872,15 @@ int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
     if (first_index) *first_index = h->count;
     if (n == 0) return RS_OK;
     RS_TRY(vt_grow_queries(h, n));
-    RS_TRY(vt_qraw_idle(h));
     const size_t qb = (size_t)h->H * h->W * n;
-    std::memcpy(h->hQraw, templates, qb);
-    RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
-    h->qrawBusy = true;
+    // the caller's array uploaded by HIP, which returns once the bytes are staged (so the
+    // caller may reuse its array at once; nothing of ours is left being read)
+    RS_HIP(hipMemcpyAsync(h->dQraw, templates, qb, hipMemcpyHostToDevice, h->stream));
     h->stagedQ = 0;  // the staging buffer now holds templates, not a query batch
     std::vector<std::pair<int, int64_t>> news;
     news.reserve(n);
     for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
     RS_TRY(vt_append_staged(h, news));   // (its copies guarded by vt_staging_idle, not a sync)
-    // the call returns with the copy from hQraw queued: the next write of hQraw waits for it
-    if (!h->evQraw) RS_HIP(hipEventCreateWithFlags(&h->evQraw, hipEventDisableTiming));
-    RS_HIP(hipEventRecord(h->evQraw, h->stream));
-    h->qrawEvRecorded = true;
     return RS_OK;
 }
 
