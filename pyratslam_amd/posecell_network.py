@@ -317,6 +317,10 @@ class PoseCellNetwork:
         """
         od = np.ascontiguousarray(np.asarray(odometry, dtype=np.float64).reshape(-1, 2))
         n = od.shape[0]
+        if n == 1 and not self._eager:
+            # one step (the ROS node's queue drain, usually): update()'s prebound call,
+            # the same library step and the same KeyError / host-control fallbacks
+            return np.array([self.update(od[0])], dtype=np.int32)
         out = np.empty((n, 3), dtype=np.int32)
         bad = ctypes.c_int(-1)
         with self._mutex:
