@@ -8,6 +8,11 @@
  * owned by the handle.  A handle is not re-entrant: callers serialise calls on
  * one handle (the Python wrapper holds a per-handle lock); distinct handles may
  * be used from different threads concurrently (ros_simulate.py:103 vs :135).
+ * Calls may return once their results have reached host memory, before the
+ * device work they queued has retired: a fault or launch error in that work is
+ * then returned (RS_ERR_HIP) by a later call on the same handle that waits for
+ * its stream -- at the latest by rs_pc_destroy / rs_vt_destroy, which always
+ * synchronise and report it after freeing the handle.
  *
  * What each entry point replaces in the reference (/root/reference/ratslam):
  *   rs_pc_create    PoseCellNetwork.__init__      posecell_network.py:24-48

@@ -19,9 +19,9 @@ SOURCES = ['rs_common.cpp', 'posecell.hip', 'view_templates.hip']
 # filter taps into register pairs and doubles the VGPRs of the conv_xy passes
 # (pc_fused_rows 90 -> 220, pc_path_rows<128> 85 -> 146), halving occupancy.
 EXTRA = {'view_templates.hip': ['-mllvm', '-amdgpu-atomic-optimizer-strategy=None'],
-         # pc_step_halo's first 7 arguments (the union image's addresses) preloaded
+         # pc_step_halo's first 9 arguments (the union image's addresses, the partial sums) preloaded
          # into scalar registers (posecell.hip, before pc_step_halo)
-         'posecell.hip': ['-fno-slp-vectorize', '-mllvm', '-amdgpu-kernarg-preload-count=7']}
+         'posecell.hip': ['-fno-slp-vectorize', '-mllvm', '-amdgpu-kernarg-preload-count=9']}
 HEADERS = [os.path.join(CSRC, 'rs_common.h'), os.path.join(INCLUDE, 'ratslam_abi.h')]
 ARCH = os.environ.get('PYRATSLAM_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

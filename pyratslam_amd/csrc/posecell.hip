@@ -2054,17 +2054,30 @@ inline int hf_pack(short lo, short hi) {
 
 // The normalisation total of a step from its per-block partials, formed by every wave
 // itself in one fixed order (so every block gets the same bits): 4 per lane, then DPP.
-__device__ inline double pc_partials_total(const double* __restrict__ part, int npart) {
+// Split in two so a kernel can issue the loads first and sum them later, behind other
+// loads already in flight (pc_step_halo).
+__device__ inline void pc_partials_issue(const double* __restrict__ part, int npart, double (&pt)[4]) {
     const int lane = threadIdx.x & 63, np1 = npart > 0 ? npart - 1 : 0;
-    double pt[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) pt[u] = part[min(lane + 64 * u, np1)];  // unconditional
+}
+__device__ inline double pc_partials_sum(const double* __restrict__ part, int npart, const double (&pt)[4]) {
+    const int lane = threadIdx.x & 63;
     double tot = 0.0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
     for (int i = lane + 256; i < npart; i += 64) tot += part[i];
     return co_wave_sum(tot);
 }
+__device__ inline double pc_partials_total(const double* __restrict__ part, int npart) {
+    double pt[4];
+    pc_partials_issue(part, npart, pt);
+    return pc_partials_sum(part, npart, pt);
+}
+// q = n / d for n, d < 2^16, d >= 2, by one high multiply with m = hf_magic(d): the error
+// of m / 2^32 against 1 / d is below 2^-32, so n * m / 2^32 stays below the next integer
+// when n < 2^32 / d
+inline unsigned hf_magic(int d) { return (unsigned)(0xFFFFFFFFull / (unsigned)d + 1ull); }
 
 // EXC: excitation only (rs_pc_excite, the step the reference runs before a LUT
 // KeyError): zero shifts, Q of the own cells stored into Uo (theta-fastest), partials.
@@ -2076,8 +2089,8 @@ __device__ inline double pc_partials_total(const double* __restrict__ part, int 
 // union, 0.84 us from the block's start to the DMA issue at 64 x 64 x 36).
 template <bool EXC>
 __global__ __launch_bounds__(HF_NT) void pc_step_halo(
-    const float* __restrict__ U, int X, int Y, int gx, int nblk, int ulo, int uext, float* __restrict__ Uo,
-    const double* __restrict__ part_in, int npart_in, double* __restrict__ part_out,
+    const float* __restrict__ U, int xy, int gxnb, int ulo, int uext, unsigned mgx, unsigned muh,
+    const double* __restrict__ part_in, int npart_in, float* __restrict__ Uo, double* __restrict__ part_out,
     unsigned long long* __restrict__ slot_prev, unsigned long long* __restrict__ slot_zero,
     const float* __restrict__ filt, int nf, PcCtlHalo ctl, SepKernel<float> k,
     unsigned long long* __restrict__ rec) {
@@ -2099,14 +2112,20 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     __shared__ int s_cnt[HF_NW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int X = xy & 0xFFFF, Y = (int)((unsigned)xy >> 16), gx = gxnb & 0xFFFF, nblk = (int)((unsigned)gxnb >> 16);
     const int tile = st_tile(blockIdx.x, nblk);
-    const int x0 = (tile % gx) * HF_T, y0 = (tile / gx) * HF_T;
+    const int ty = (int)__umulhi((unsigned)tile, mgx);   // tile / gx (hf_magic)
+    const int x0 = (tile - ty * gx) * HF_T, y0 = ty * HF_T;
     const int tw = min(HF_T, X - x0), tht = min(HF_T, Y - y0);
     const int cux = (short)(ulo & 0xFFFF), cuy = ulo >> 16;   // the union's origin (centred shifts)
     const int UW = uext & 0xFFFF, UH = uext >> 16, nu = UW * UH;
     const int ux0 = co_wrap(x0 - 2 * HALF + cux, X), uy0 = co_wrap(y0 - 2 * HALF + cuy, Y);
     const bool dma = nu <= HF_UMAX;
     PC_STAMP(7, 0);
+    // the partial sums of the state entering the step, issued ahead of the union image so
+    // they land first and the total is formed while the image is in flight
+    double pt[4];
+    pc_partials_issue(part_in, npart_in, pt);
     // 1. the union image, issued first: piece p = tid + HF_NT * r is 16-byte piece p % NV
     //    of union cell p / NV (cells row-major, UH per row), landing at s_b + 4p
     if (dma) {
@@ -2117,8 +2136,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         // gr * Y carried incrementally (the union row advances by dU or dU + 1 < X per
         // round and UW <= X, so one wrap suffices), a 32-bit byte offset from the state's
         // base (n * 4 <= INT_MAX, pc_halo_fit) by a 24-bit multiply (cells < 2^24)
-        const int npc = nu * NV, dU = DC / UH, dV = DC - dU * UH, XY = X * Y;
-        int c = tid / NV, l4 = tid - c * NV, ui = c / UH, vi = c - ui * UH;
+        const int npc = nu * NV, dU = (int)__umulhi((unsigned)DC, muh), dV = DC - dU * UH, XY = X * Y;
+        int c = tid / NV, l4 = tid - c * NV, ui = (int)__umulhi((unsigned)c, muh), vi = c - ui * UH;
         int rb = ux0 + ui;
         rb = (rb >= X ? rb - X : rb) * Y;
 #pragma unroll
@@ -2155,8 +2174,19 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     const float fr = tid < nf * FT ? filt[tid] : 0.f;
     static_assert(RT_NFMAX * FT <= HF_NT, "one filter tap per thread");
     if (tid < TH) s_fo[tid] = ctl.fo[tid] * ST_FTP;
-    const PcNorm<float> nrm(pc_partials_total(part_in, npart_in));
+    const PcNorm<float> nrm(pc_partials_sum(part_in, npart_in, pt));
     if (tid < nf * FT) s_ftab[(tid / FT) * ST_FTP + tid % FT] = fr;
+    // the tap pairs and the wrap flag (kernel arguments beyond the preloaded ones) in
+    // registers before the barrier: hipcc otherwise loads them after it, a scalar round
+    // trip at the head of phase 2
+    hf_f2 gei[FL];
+#pragma unroll
+    for (int t = 0; t < FL; ++t) {
+        gei[t] = hf_f2{k.ge[t], k.gi[t]};
+        asm volatile("" : "+s"(gei[t]));
+    }
+    int cwrap = ctl.wrap;
+    asm volatile("" : "+s"(cwrap));
     if (slot_zero != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += HF_NT) st_wt(&slot_zero[i], 0ull);  // the next launch max-reduces into them
     if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces have landed
@@ -2169,11 +2199,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     hf_f2* s_tw = reinterpret_cast<hf_f2*>(s_t);
     unsigned long long bk = 0ull;
     const bool want_key = slot_prev != nullptr;
-    hf_f2 gei[FL];
-#pragma unroll
-    for (int t = 0; t < FL; ++t) gei[t] = hf_f2{k.ge[t], k.gi[t]};
     PC_STAMP(11, 0);
-    if (dma && !ctl.wrap) {
+    if (dma && !cwrap) {
         // the common case, read straight from the union image [cell][layer]: wave w < 8
         // takes window rows 4(w&3) .. +3 (a lane per window cell) through the layers
         // [18(w>>2), +18).  Layer j's window cell (rx, ry) is union cell (rx + sx_j,
@@ -2340,7 +2367,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 }
             }
         };
-        if (ctl.wrap) {
+        if (cwrap) {
 #pragma unroll 1
             for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::true_type{});
         } else {
@@ -2567,18 +2594,34 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
 // The end of a halo-form call: the normalised state P = U * (1/t) of the last step
 // (written back, so the handle's state is normalised between calls), its argmax key
 // per block into the last step's slots, optionally the float64 C-order volume into a
-// pinned host array (readback='eager'), and -- the last block to finish, told by an
-// agent-scope counter -- the keys of all nexp steps into the host result words (the
-// export kernel of the other forms, folded in: one launch fewer per call).
+// pinned host array (readback='eager'), and the keys of the call's nexp steps for the
+// host (the export kernel of the other forms, folded in: one launch fewer per call):
+// block 0 stores the words of steps 0 .. nexp-2, whose slots earlier launches of the
+// call completed, and every block stores its own key of the last step into bkey[block],
+// which the host max-reduces once it has waited for the launch.  No block reads what
+// another block of this launch wrote, so the kernel needs no intra-launch hand-off (the
+// round-5 form handed the last step's slots to the block that counted last through an
+// agent-scope counter, outside the memory model's release/acquire).
 __global__ __launch_bounds__(256) void pc_halo_finish(
     const float* U, float* P,  // may be one buffer: each element is read, then written, by one thread
     int n4, const double* __restrict__ part,
     int npart, unsigned long long* __restrict__ slot, const unsigned long long* __restrict__ res,
-    int nexp, unsigned* __restrict__ counter, unsigned long long* __restrict__ host,
-    double* __restrict__ xp, int nbytes, int fence, unsigned* __restrict__ flag, unsigned seq) {
+    int nexp, unsigned long long* __restrict__ host, unsigned long long* __restrict__ bkey,
+    double* __restrict__ xp, int nbytes, unsigned* __restrict__ flag, unsigned seq) {
     __shared__ unsigned long long s_bk[4];
-    __shared__ int s_last;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (nexp > 1 && blockIdx.x == 0) {
+        // steps 0 .. nexp-2: each step's max of its RES_SLOTS slots (filled by the launches
+        // before this one) straight into the pinned host words
+        for (int s = wave; s < nexp - 1; s += 4) {
+            const unsigned long long* r = res + (size_t)s * RES_SLOTS;
+            unsigned long long m = 0ull;
+#pragma unroll
+            for (int q = 0; q < RES_SLOTS / 64; ++q) m = max(m, r[lane + 64 * q]);
+            m = co_wave_max(m);
+            if (lane == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const PcNorm<float> nrm(pc_partials_total(part, npart));
     unsigned long long bk = 0ull;
     typedef double d2 __attribute__((ext_vector_type(2)));
@@ -2608,43 +2651,12 @@ __global__ __launch_bounds__(256) void pc_halo_finish(
     if (tid == 0) {
         bk = max(max(s_bk[0], s_bk[1]), max(s_bk[2], s_bk[3]));
         if (slot) atomicMax(slot + (blockIdx.x & (RES_SLOTS - 1)), bk);
-        if (flag) {
+        if (bkey) __hip_atomic_store(bkey + blockIdx.x, bk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (flag) {   // after the block's volume and its key
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(flag + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        s_last = 0;
-        if (nexp > 0) {
-            // The hand-off of the keys to the block that counts last: the key is an
-            // agent-scope atomic (performed at memory, never held in an L2), each block's
-            // one lane waits for it (vmcnt(0)) before its counter add, the last adder
-            // learns it from the value its add returns, and it reads the slots with sc1
-            // loads only -- the hand-off MI355X_MICROARCH.md measures valid without an
-            // acquire ("Hand-offs measured with sc1 loads in place of the acquire", first
-            // row; not an architectural guarantee).  fence = 1 adds the model's agent
-            // release / acquire pair (RS_PC_HALO_FENCE=1): a buffer_wbl2 in every block,
-            // +1.5 us per update() at 64x64x36 (tools/pc_call_anatomy.py, round 5).
-            if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            s_last = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     gridDim.x - 1;
-            if (fence && s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        }
-    }
-    __syncthreads();
-    if (s_last) {
-        // every block's key is in: each step's max of its RES_SLOTS slots (sc1 loads,
-        // past this CU's L1) straight into the pinned host words
-        for (int s = wave; s < nexp; s += 4) {
-            const unsigned long long* r = res + (size_t)s * RES_SLOTS;
-            unsigned long long m = 0ull;
-#pragma unroll
-            for (int q = 0; q < RES_SLOTS / 64; ++q)
-                m = max(m, __hip_atomic_load(r + lane + 64 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            m = co_wave_max(m);
-            if (lane == 0) __hip_atomic_store(host + s, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        if (tid == 0) st_wt(counter, 0u);  // for the next call
     }
 }
 
@@ -2819,16 +2831,7 @@ __device__ inline size_t pc_layer_major(size_t e, int X, int Y, int TH) {
     return ((size_t)k * X + i) * Y + j;
 }
 
-template <typename T>
-__global__ void pc_export_kernel(const T* __restrict__ P, double* __restrict__ out, int X, int Y,
-                                 int TH, int thfast) {
-    const size_t n = (size_t)X * Y * TH;
-    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n;
-         e += (size_t)gridDim.x * blockDim.x)
-        out[e] = (double)P[thfast ? e : pc_layer_major(e, X, Y, TH)];
-}
-
-// The same export with 16-byte stores (two consecutive cells per thread): a wave's
+// The float64 C-order export with 16-byte stores (two consecutive cells per thread): a wave's
 // stores are 1 KiB contiguous, the unit host writes over PCIe favour.  out is
 // 16-byte aligned (rs_host_alloc / hipMalloc); an odd last cell goes alone.
 // flag (host memory the host polls instead of the stream's completion, pc_poll_flags):
@@ -2944,12 +2947,13 @@ struct rs_pc {
                             // P and Q are then theta-fastest (C order (x, y, th))
     bool halo = false;      // one launch per step (RS_PC_FORM=halo): HF_T x HF_T tiles through all
                             // layers, the excitation recomputed on each tile's halo; P theta-fastest
-    unsigned* dCounter = nullptr;  // pc_halo_finish's last-block counter
     unsigned long long* dRec = nullptr;  // halo: the last launch's per-block (key of max U, near count)
     unsigned long long* hRec = nullptr;  // ... for a one-step call: pinned host records (hRecDev on the device)
     unsigned long long* hRecDev = nullptr;
     unsigned* hFlag = nullptr;      // halo: pc_halo_finish's per-block flags (pinned; eager readback polls)
     unsigned* hFlagDev = nullptr;
+    unsigned long long* hKey = nullptr;     // halo: pc_halo_finish's per-block keys of a call's last step (pinned)
+    unsigned long long* hKeyDev = nullptr;
     unsigned flagSeq = 0u;
     bool haloPend = false;  // halo: the state is U, unnormalised, in buffer haloCur (0 dP, 1 dQ) with
     int haloCur = 0, haloPart = 0;  // its partial sums in half haloPart of dPart (pc_halo_settle)
@@ -3193,15 +3197,9 @@ bool pc_flags_ok(const rs_pc* h, int nb) {
 }
 // The export kernel's grid when its flags are polled: at most 128 blocks, each thread
 // storing a few 16-byte pieces (fewer blocks, fewer flags; 64x64x36 rows-form read 32-36
-// us at 32-128 blocks against 36-37 at 289, within the boxes' spread; RS_PC_XFLAG_NB
-// overrides, tools/node_step.py, round 5)
-int pc_xflag_nb(int nb) {
-    static const int cap = [] {
-        const char* e = std::getenv("RS_PC_XFLAG_NB");
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 128;
-    }();
-    return std::min(nb, cap);
-}
+// us at 32-128 blocks against 36-37 at 289, within the boxes' spread, tools/node_step.py,
+// round 5)
+int pc_xflag_nb(int nb) { return std::min(nb, 128); }
 
 // pc_halo_export's last-step rule on the host, over records in pinned host memory: the
 // largest key, or RES_AMBIG when another cell may round to the same scaled value; RES_NONE
@@ -3236,8 +3234,8 @@ int pc_halo_settle(rs_pc* h) {
     float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
     const int n4 = (int)(h->n / 4), nb = std::min(1024, (n4 + 255) / 256);
     hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
-                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
-                       nullptr, nullptr, (int)(h->n * sizeof(float)), 0, nullptr, 0u);
+                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, nullptr,
+                       nullptr, nullptr, (int)(h->n * sizeof(float)), nullptr, 0u);
     RS_HIP(hipGetLastError());
     h->haloPend = false;
     h->haloCur = 0;
@@ -3261,8 +3259,8 @@ int pc_halo_settle_read(rs_pc* h, double* xp_dev, bool* done) {
     const bool fl = pc_flags_ok(h, nb);
     const unsigned seq = fl ? pc_next_seq(h) : 0u;
     hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[h->haloCur], buf[0], n4,
-                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, h->dCounter,
-                       nullptr, xp_dev, (int)(h->n * sizeof(float)), 0, fl ? h->hFlagDev : nullptr, seq);
+                       h->dPart + (size_t)h->haloPart * h->nPart, h->nPart, nullptr, nullptr, 0, nullptr,
+                       nullptr, xp_dev, (int)(h->n * sizeof(float)), fl ? h->hFlagDev : nullptr, seq);
     RS_HIP(hipGetLastError());
     h->haloPend = false;
     h->haloCur = 0;
@@ -3288,33 +3286,13 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     const bool pk = h->profiling && h->profKernels;
     if (pk) RS_TRY(pc_ensure_events(h, (size_t)2 * n + 2));
     for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
-    // RS_PC_HALO_SETTLE=1: every call ends normalised (the round-4 sequence, A/B);
-    // RS_PC_HALO_EXPORT=kernel: the finishing kernel's keys exported by a separate launch
-    // instead of its last block; RS_PC_HALO_FENCE=1: that hand-off fenced;
     // RS_PC_HALO_POLL=0: a one-step call waits for the kernel's completion signal instead
     // of returning once every block's record has reached host memory (below)
-    static const bool settle_env = [] {
-        const char* e = std::getenv("RS_PC_HALO_SETTLE");
-        return e && std::strcmp(e, "1") == 0;
-    }();
-    static const bool export_last = [] {   // (node step, eager: 28.2 vs 29.3 us at 21x21x36, round 5)
-        const char* e = std::getenv("RS_PC_HALO_EXPORT");
-        return !(e && std::strcmp(e, "kernel") == 0);
-    }();
     const bool poll_env = halo_poll_env();
-    static const int fence = [] {
-        const char* e = std::getenv("RS_PC_HALO_FENCE");
-        return e && std::strcmp(e, "1") == 0 ? 1 : 0;
-    }();
-    static const bool rec_device = [] {
-        const char* e = std::getenv("RS_PC_HALO_REC");
-        return e && std::strcmp(e, "device") == 0;
-    }();
-    const bool lazy = h->exportDev == nullptr && !settle_env && !h->haloSettleAlways;
+    const bool lazy = h->exportDev == nullptr && !h->haloSettleAlways;
     // a one-step call: the blocks' records go straight to pinned host memory and the host
-    // reduces them after its sync (no export launch; RS_PC_HALO_REC=device: the export
-    // kernel, as for batches)
-    const bool host_rec = lazy && n == 1 && h->hRec && !rec_device;
+    // reduces them after its wait (no export launch)
+    const bool host_rec = lazy && n == 1 && h->hRec;
     if (host_rec) std::memset(h->hRec, 0, sizeof(unsigned long long) * 2 * h->nPart);
     if (h->profiling) RS_HIP(hipEventRecord(h->ev0, h->stream));
     float* buf[2] = {static_cast<float*>(h->dP), static_cast<float*>(h->dQ)};
@@ -3329,9 +3307,10 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                                       : h->dPart + (size_t)(pend ? h->haloPart : 0) * h->nPart;
         const int npart_in = s > 0 || pend ? h->nPart : 0;
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
-        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[(c0 + s) & 1], h->X, h->Y,
-                           h->cgx, (int)grid.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), buf[(c0 + s + 1) & 1],
-                           part_in, npart_in, h->dPart + (size_t)((p0 + s) & 1) * h->nPart,
+        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[(c0 + s) & 1],
+                           hf_pack(h->X, h->Y), hf_pack(h->cgx, grid.x), hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh),
+                           hf_magic(h->cgx), hf_magic(c.uh), part_in, npart_in, buf[(c0 + s + 1) & 1],
+                           h->dPart + (size_t)((p0 + s) & 1) * h->nPart,
                            s == 0 ? nullptr : h->dRes + (size_t)(s - 1) * RES_SLOTS,
                            h->dRes + (size_t)s * RES_SLOTS, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
                            lazy && s == n - 1 ? (host_rec ? h->hRecDev : h->dRec) : nullptr);
@@ -3343,18 +3322,22 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     // an eager readback the host may poll for (per-block flags behind a system-scope release)
     const bool flag_poll = xp_poll_ok(h, n, poll_env);
     const unsigned seq = flag_poll ? pc_next_seq(h) : 0u;
+    // own export: block 0 stores the words of steps 0 .. n-2, every block its key of step
+    // n-1 into hKey, reduced here once the launch has been waited for
     auto finish = [&](int nexp_own, double* xp) -> int {
         const bool fl = flag_poll && xp != nullptr;
+        if (nexp_own > 0) std::memset(h->hKey, 0, sizeof(unsigned long long) * nb);
         hipLaunchKernelGGL(pc_halo_finish, dim3(nb), dim3(256), 0, h->stream, buf[cl], buf[0], n4,
                            h->dPart + (size_t)pl * h->nPart, h->nPart, h->dRes + (size_t)(n - 1) * RES_SLOTS,
-                           h->dRes, nexp_own, h->dCounter, h->hResDev, xp, (int)(h->n * sizeof(float)), fence,
-                           fl ? h->hFlagDev : nullptr, seq);
+                           h->dRes, nexp_own, h->hResDev, nexp_own > 0 ? h->hKeyDev : nullptr, xp,
+                           (int)(h->n * sizeof(float)), fl ? h->hFlagDev : nullptr, seq);
         RS_HIP(hipGetLastError());
         h->haloPend = false;
         h->haloCur = 0;
         return RS_OK;
     };
     if (pk) RS_HIP(hipEventRecord(h->evPool[2 * n], h->stream));
+    bool own_export = false;
     if (lazy) {
         if (!h->dbgSkipExport && !host_rec) {
             hipLaunchKernelGGL(pc_halo_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
@@ -3365,7 +3348,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
         h->haloCur = cl;
         h->haloPart = pl;
     } else {
-        const bool own_export = !h->dbgSkipExport && n <= HF_EXP_MAX && export_last;
+        own_export = !h->dbgSkipExport && n <= HF_EXP_MAX;
         RS_TRY(finish(own_export ? n : 0, h->exportDev));
         if (!h->dbgSkipExport && !own_export) {
             hipLaunchKernelGGL(pc_res_export, dim3(n < 1024 ? n : 1024), dim3(64), 0, h->stream, h->dRes, n,
@@ -3392,7 +3375,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     if (flag_poll && !lazy && !skipped) {
         // the eager readback: every finishing block's flag (its volume slice released at
         // system scope before it), then every step's key word
-        polled = pc_poll_flags(h, nb, seq) && pc_poll_words(h, 0, n);
+        polled = pc_poll_flags(h, nb, seq) && pc_poll_words(h, 0, n - 1);
     }
     if (lazy && !skipped && poll_env && !h->profiling && n <= HF_POLL_MAX) {
         if (host_rec) {
@@ -3408,6 +3391,15 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
     }
     if (!polled) RS_HIP(hipStreamSynchronize(h->stream));
     if (host_rec && !skipped) h->hRes[n - 1] = halo_key_from_records(h->hRec, (int)grid.x);
+    if (own_export) {   // the finishing blocks' keys of the last step (a key is never 0)
+        unsigned long long m = 0ull;
+        bool all = true;
+        for (int b = 0; b < nb; ++b) {
+            all &= h->hKey[b] != 0ull;
+            m = std::max(m, h->hKey[b]);
+        }
+        h->hRes[n - 1] = all ? m : RES_NONE;
+    }
     if (lazy && !skipped && h->hRes[n - 1] == RES_AMBIG) {
         // a cell within HF_NEAR of the last step's peak: key the normalised state itself
         // (its slots were zeroed by the last launch and nothing has reduced into them)
@@ -3596,13 +3588,8 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
     // Batches: the column form takes each step's control as kernel arguments too (its
     // path kernel then starts its window loads without a global round trip for the
     // shifts: 128x128x72 27.5 -> 27.1 us per step with the filter table staged behind
-    // the window); the other forms read the device ring (RS_PC_CTL=ring|inline overrides)
-    static const int ctl_env = [] {
-        const char* e = std::getenv("RS_PC_CTL");
-        return !e ? -1 : std::strcmp(e, "inline") == 0 ? 1 : std::strcmp(e, "ring") == 0 ? 0 : -1;
-    }();
-    const bool batch_inline = ctl_env >= 0 ? ctl_env == 1 : h->cols;
-    const bool inline_ctl = (n == 1 || batch_inline) && h->TH <= CTL_INLINE_MAX;
+    // the window); the other forms read the device ring
+    const bool inline_ctl = (n == 1 || h->cols) && h->TH <= CTL_INLINE_MAX;
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
@@ -3852,7 +3839,10 @@ int pc_cols_set(rs_pc* h, int kc) {
 // windows without self-overlap, the filter table in LDS, 32-bit buffer offsets.
 bool pc_halo_fit(const rs_pc* h) {
     // (the union's origin and extent travel as 16-bit fields: make_ctl_halo, hf_pack)
+    // (so do the grid, the tile count and the block count of pc_step_halo; tile / gx is a
+    // high multiply valid below 2^16, hf_magic)
     return h->esz == 4 && h->TH == HF_TH && h->X >= HF_W && h->Y >= HF_W && h->X <= 32767 && h->Y <= 32767 &&
+           (size_t)((h->X + HF_T - 1) / HF_T) * ((h->Y + HF_T - 1) / HF_T) <= 65535 &&
            h->nf <= RT_NFMAX && h->n * sizeof(float) <= (size_t)INT_MAX;
 }
 
@@ -4058,8 +4048,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
     PC_ALLOC(hipHostMalloc(&h->hFlag, sizeof(unsigned) * HF_FLAGS, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(h->hFlag, 0, sizeof(unsigned) * HF_FLAGS);
     PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hFlagDev), h->hFlag, 0));
-    PC_ALLOC(hipMalloc(&h->dCounter, sizeof(unsigned)));
-    PC_ALLOC(hipMemsetAsync(h->dCounter, 0, sizeof(unsigned), h->stream));
+    if (h->halo) {
+        PC_ALLOC(hipHostMalloc(&h->hKey, sizeof(unsigned long long) * HF_FLAGS,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+        PC_ALLOC(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hKeyDev), h->hKey, 0));
+    }
     PC_ALLOC(hipMalloc(&h->dBmax, h->esz * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dBidx, sizeof(unsigned) * h->nBmaxCap));
     PC_ALLOC(hipMalloc(&h->dTmp, sizeof(double) * h->n));
@@ -4090,9 +4083,11 @@ int rs_pc_create(int X, int Y, int TH, const rs_pc_params* p, int device, rs_pc*
 int rs_pc_destroy(rs_pc* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    // the handle's last queued work: a fault or launch error the early-returning calls
+    // left on the stream is reported here instead of being dropped
+    const hipError_t se = h->stream ? hipStreamSynchronize(h->stream) : hipSuccess;
     if (h->hRead) (void)hipHostFree(h->hRead);
-    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, (void*)h->dCounter, (void*)h->dRec, h->dBmax,
+    for (void* p : {h->dP, h->dQ, h->dFilt, (void*)h->dPart, (void*)h->dRec, h->dBmax,
                     (void*)h->dBidx, h->dArgV,
                     (void*)h->dArgI,
                     (void*)h->dRes, (void*)h->dCtl, (void*)h->dTmp, (void*)h->dScalar})
@@ -4100,12 +4095,14 @@ int rs_pc_destroy(rs_pc* h) {
     if (h->hRes) (void)hipHostFree(h->hRes);
     if (h->hRec) (void)hipHostFree(h->hRec);
     if (h->hFlag) (void)hipHostFree(h->hFlag);
+    if (h->hKey) (void)hipHostFree(h->hKey);
     if (h->hCtl) (void)hipHostFree(h->hCtl);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     for (hipEvent_t e : h->evPool) (void)hipEventDestroy(e);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
+    RS_CHECK(se == hipSuccess, RS_ERR_HIP, "work queued before rs_pc_destroy failed: %s", hipGetErrorString(se));
     return RS_OK;
 }
 
@@ -4140,9 +4137,9 @@ int rs_pc_excite(rs_pc* h) {
         c.uw = (short)HF_W;
         c.uh = (short)HF_W;
         hipLaunchKernelGGL((pc_step_halo<true>), dim3(h->cgx * h->cgy), dim3(HF_NT), 0, h->stream,
-                           static_cast<const float*>(h->dP), h->X, h->Y, h->cgx, h->cgx * h->cgy,
-                           hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), static_cast<float*>(h->dQ), h->dPart, 0,
-                           h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
+                           static_cast<const float*>(h->dP), hf_pack(h->X, h->Y), hf_pack(h->cgx, h->cgx * h->cgy),
+                           hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), hf_magic(h->cgx), hf_magic(c.uh), h->dPart, 0,
+                           static_cast<float*>(h->dQ), h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,
                            nullptr);
         RS_HIP(hipGetLastError());
         hipLaunchKernelGGL((pc_scale_kernel<float>), dim3(64), dim3(NT), 0, h->stream,
@@ -4345,28 +4342,10 @@ int rs_pc_read(rs_pc* h, double* host) {
     RS_HIP(hipSetDevice(h->device));
     // The export kernel writes the float64 C-order volume straight into pinned host
     // memory (one launch, no copy engine), then the host copies it into the caller's
-    // array; RS_PC_READ=dma exports to HBM and copies with hipMemcpyAsync instead.
-    static const bool dma = [] {
-        const char* e = std::getenv("RS_PC_READ");
-        return e && std::strcmp(e, "dma") == 0;
-    }();
-    if (!dma && !h->hRead) {
+    // array.
+    if (!h->hRead) {
         RS_HIP(hipHostMalloc(&h->hRead, sizeof(double) * h->n, hipHostMallocMapped | hipHostMallocCoherent));
         RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hReadDev), h->hRead, 0));
-    }
-    if (dma) {
-        RS_TRY(pc_halo_settle(h));  // (halo: a state a call left unnormalised)
-        const int nb = (int)std::min<size_t>(1024, (h->n + NT - 1) / NT);
-        if (h->prec == RS_PREC_F32)
-            hipLaunchKernelGGL((pc_export_kernel<float>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const float*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)pc_thfast(h));
-        else
-            hipLaunchKernelGGL((pc_export_kernel<double>), dim3(nb), dim3(NT), 0, h->stream,
-                               static_cast<const double*>(h->dP), h->dTmp, h->X, h->Y, h->TH, (int)pc_thfast(h));
-        RS_HIP(hipGetLastError());
-        RS_HIP(hipMemcpyAsync(host, h->dTmp, sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
-        RS_HIP(hipStreamSynchronize(h->stream));
-        return RS_OK;
     }
     RS_TRY(pc_read_volume(h, h->hReadDev));
     std::memcpy(host, h->hRead, sizeof(double) * h->n);

@@ -790,14 +790,20 @@ void vt_scan_plane_kernel(const uint4* __restrict__ planes, const uint32_t* __re
             // keys are agent-scope atomics (performed at memory, never held in an L2), each
             // wave waits for its own (vmcnt(0)) before the block's counter add, the last
             // adder learns it from the add's return value and reads the keys with sc1
-            // loads only -- the hand-off pc_halo_finish uses (MI355X_MICROARCH.md's
-            // hand-off rows), then stores them into the pinned host words and resets them.
+            // loads, then stores them into the pinned host words and resets them.
+            // The model's agent-scope release before each block's counter add and acquire
+            // in the last block frame the hand-off (a release fence after the block barrier
+            // is cumulative over the waves' atomics; the acquire is one cache invalidate in
+            // one block of the launch).
             __shared__ int s_last;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (threadIdx.x == 0)
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 s_last = __hip_atomic_fetch_add(out.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                          gridDim.x - 1;
+                if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
             __syncthreads();
             if (s_last) {
                 for (int i = threadIdx.x; i < nq; i += blockDim.x) {
@@ -1054,8 +1060,8 @@ int vt_grow_lib(rs_vt* h, int64_t need_slots) {
     return RS_OK;
 }
 
-// hQraw (pinned) is read by a queued copy (RS_VT_STAGE=pinned) or, for small batches, in
-// place by the plane kernel: before the host writes or frees it again that work must
+// hQraw (pinned) is read by a queued copy (frames, float batches) or, for small batches,
+// in place by the plane kernel: before the host writes or frees it again that work must
 // have run.  Every call that stages into it waits for its keys before returning
 // (vt_fetch_keys clears the flag); after an error between the staging and that wait the
 // stream is synchronised here.  (rs_vt_add uploads the caller's array directly.)
@@ -1165,12 +1171,9 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
     const size_t qb = (size_t)h->H * h->W * nq;
     // larger batches: HIP's own upload of the caller's (pageable) array, which returns
     // once the bytes are staged (per-batch PCIe-inclusive rate 4.04-4.12 against 3.44-3.54
-    // G compares/s through our memcpy into pinned staging, round 5); RS_VT_STAGE=pinned:
-    // the memcpy
-    static const bool direct = [] {
-        const char* e = std::getenv("RS_VT_STAGE");
-        return !(e && std::strcmp(e, "pinned") == 0);
-    }();
+    // G compares/s through our memcpy into pinned staging, round 5).  The call waits for
+    // its keys, which the scan stores after the copy has run, so a pinned caller array is
+    // no longer read when it returns.
     if (h->planar && nq <= VT_ZC_MAX && vt_zc_env()) {
         std::memcpy(h->hQraw, queries, qb);
         h->qrawBusy = true;
@@ -1179,13 +1182,7 @@ int vt_stage_queries(rs_vt* h, int nq, const uint8_t* queries) {
         RS_HIP(hipGetLastError());
         return RS_OK;
     }
-    if (direct) {
-        RS_HIP(hipMemcpyAsync(h->dQraw, queries, qb, hipMemcpyHostToDevice, h->stream));
-        return vt_build_forms(h, nq);
-    }
-    std::memcpy(h->hQraw, queries, qb);
-    h->qrawBusy = true;
-    RS_HIP(hipMemcpyAsync(h->dQraw, h->hQraw, qb, hipMemcpyHostToDevice, h->stream));
+    RS_HIP(hipMemcpyAsync(h->dQraw, queries, qb, hipMemcpyHostToDevice, h->stream));
     return vt_build_forms(h, nq);
 }
 
@@ -1648,12 +1645,8 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
         } else {
             // groups of about a quarter of the call (2 .. VT_UP_GROUP batches): the first
             // group's upload is the only one not hidden behind a scan, and a scan launch of
-            // >= 2 batches keeps the fused launch's efficiency (RS_VT_UP_GROUP overrides)
-            static const int gb_env = [] {
-                const char* e = std::getenv("RS_VT_UP_GROUP");
-                return e ? std::atoi(e) : 0;
-            }();
-            const int gb = gb_env > 0 ? std::min(nb, gb_env) : std::min(nb, std::max(2, std::min(VT_UP_GROUP, nb / 4)));
+            // >= 2 batches keeps the fused launch's efficiency
+            const int gb = std::min(nb, std::max(2, std::min(VT_UP_GROUP, nb / 4)));
             if (!h->ustream) {
                 RS_HIP(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
                 for (int i = 0; i < 2; ++i) {
@@ -1799,9 +1792,6 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
         const int by_lds = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) : per_cu;
         const int api = per_cu;
         per_cu = std::max(1, std::min({api, by_vgpr, by_lds}));
-        if (std::getenv("RS_VT_DEBUG"))
-            std::fprintf(stderr, "plane scan: %d blocks/CU (api %d, vgpr %d [%d regs], lds %d) x %d CUs\n",
-                         per_cu, api, by_vgpr, fa.numRegs, by_lds, cus);
         h->planeSlots = std::max(1, per_cu * cus);
     }
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -1826,9 +1816,14 @@ int rs_vt_create(int H, int W, int max_offset, uint64_t thr, int64_t capacity, i
 int rs_vt_destroy(rs_vt* h) {
     if (!h) return RS_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
-    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
-    if (h->ustream) (void)hipStreamSynchronize(h->ustream);
+    // the handle's last queued work: a fault or launch error the early-returning calls
+    // left on a stream is reported here instead of being dropped
+    hipError_t se = hipSuccess;
+    for (hipStream_t st : {h->stream, h->cstream, h->ustream})
+        if (st) {
+            const hipError_t e = hipStreamSynchronize(st);
+            if (se == hipSuccess) se = e;
+        }
     if (h->comm) (void)ncclCommDestroy(h->comm);
     for (void* p : {(void*)h->dLib, (void*)h->dQraw, (void*)h->dQf, (void*)h->dQsum, (void*)h->dBest,
                     (void*)h->dSrc, (void*)h->dDst, (void*)h->dCand, (void*)h->dMat, (void*)h->dLibP,
@@ -1855,6 +1850,7 @@ int rs_vt_destroy(rs_vt* h) {
     if (h->ustream) (void)hipStreamDestroy(h->ustream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
+    RS_CHECK(se == hipSuccess, RS_ERR_HIP, "work queued before rs_vt_destroy failed: %s", hipGetErrorString(se));
     return RS_OK;
 }
 
@@ -1873,14 +1869,25 @@ int rs_vt_add(rs_vt* h, int n, const uint8_t* templates, int64_t* first_index) {
     if (n == 0) return RS_OK;
     RS_TRY(vt_grow_queries(h, n));
     const size_t qb = (size_t)h->H * h->W * n;
-    // the caller's array uploaded by HIP, which returns once the bytes are staged (so the
-    // caller may reuse its array at once; nothing of ours is left being read)
-    RS_HIP(hipMemcpyAsync(h->dQraw, templates, qb, hipMemcpyHostToDevice, h->stream));
+    // A pageable array is uploaded by HIP, which returns once the bytes are staged in its
+    // own buffers.  Pinned or registered host memory, or device memory, is read by the
+    // DMA engine while the copy runs, after this call would return: those sources are
+    // waited for below, so in every case the caller may reuse or free its array at once.
+    hipPointerAttribute_t attr{};
+    const bool direct_dma = hipPointerGetAttributes(&attr, templates) == hipSuccess &&
+                            (attr.type == hipMemoryTypeHost || attr.type == hipMemoryTypeDevice ||
+                             attr.type == hipMemoryTypeManaged);
+    (void)hipGetLastError();  // a pageable pointer is not an error
+    RS_HIP(hipMemcpyAsync(h->dQraw, templates, qb,
+                          attr.type == hipMemoryTypeDevice && direct_dma ? hipMemcpyDeviceToDevice
+                                                                         : hipMemcpyHostToDevice,
+                          h->stream));
     h->stagedQ = 0;  // the staging buffer now holds templates, not a query batch
     std::vector<std::pair<int, int64_t>> news;
     news.reserve(n);
     for (int i = 0; i < n; ++i) news.emplace_back(i, h->count + i);
     RS_TRY(vt_append_staged(h, news));   // (its copies guarded by vt_staging_idle, not a sync)
+    if (direct_dma) RS_HIP(hipStreamSynchronize(h->stream));
     return RS_OK;
 }
 

@@ -171,12 +171,14 @@ class PoseCellNetwork:
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
+        st = 0
         if self._h is not None and self._h.value:
-            self._lib.rs_pc_destroy(self._h)
+            st = self._lib.rs_pc_destroy(self._h)   # (reports an error of queued work)
         self._h = None
         if getattr(self, '_pinned', None) is not None:
             self._pinned.close()
             self._pinned = None
+        _lib.check(st)
 
     def __del__(self):
         try:

@@ -153,9 +153,11 @@ class ViewTemplates:
 
     # -- lifetime ---------------------------------------------------------------
     def close(self):
+        st = 0
         if getattr(self, '_h', None) is not None and self._h.value:
-            self._lib.rs_vt_destroy(self._h)
+            st = self._lib.rs_vt_destroy(self._h)   # (reports an error of queued work)
         self._h = None
+        _lib.check(st)
 
     def __del__(self):
         try:

@@ -158,6 +158,52 @@ def test_sequential_batch_equals_oracle_sequence(vtmod):
     assert np.array_equal(np.stack([t.template for t in lib.templates]), np.stack(ref.templates))
 
 
+def test_add_from_pinned_or_device_memory_then_overwrite(vtmod):
+    """rs_vt_add from pinned host memory (rs_host_alloc) and from device memory: the DMA
+    engine reads those sources directly, so the call waits for its copy before returning;
+    the caller overwrites or frees the array at once and the stored templates are still
+    the bytes it passed (every pair score against the oracle, and the bytes read back)."""
+    import ctypes
+    from pyratslam_amd import _lib
+    lib_np = V.synthetic_library(192, 64, 32, seed=31)
+    ll = _lib.require_device()
+    p = ctypes.c_void_p()
+    _lib.check(ll.rs_host_alloc(lib_np.nbytes, ctypes.byref(p)))
+    try:
+        pinned = np.frombuffer((ctypes.c_uint8 * lib_np.nbytes).from_address(p.value),
+                               dtype=np.uint8).reshape(lib_np.shape)
+        lib = vtmod.ViewTemplates._from_shape((64, 32), 45000)
+        for i in range(0, 128, 32):
+            pinned[:32] = lib_np[i:i + 32]
+            lib.add(pinned[:32])
+            pinned[:32] = 0xA5          # overwritten the moment add() returns
+        pinned[:] = 0x5A
+    finally:
+        _lib.check(ll.rs_host_free(p))
+    hip = ctypes.CDLL('libamdhip64.so')   # device memory as a caller might hold it
+    src = np.ascontiguousarray(lib_np[128:])
+    dev = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(dev), ctypes.c_size_t(src.nbytes)) == 0
+    try:
+        assert hip.hipMemcpy(dev, src.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(src.nbytes), 1) == 0
+        first = ctypes.c_int64()
+        with lib._mutex:
+            _lib.check(lib._lib.rs_vt_add(lib._h, 64, ctypes.cast(dev, ctypes.POINTER(ctypes.c_uint8)),
+                                          ctypes.byref(first)))
+        assert hip.hipMemset(dev, 0x3C, ctypes.c_size_t(src.nbytes)) == 0
+        assert hip.hipDeviceSynchronize() == 0
+    finally:
+        hip.hipFree(dev)
+    assert first.value == 128
+    queries, _ = V.synthetic_queries(lib_np, 24, seed=32)
+    ref = np.stack([V.vt_scores_library(lib_np, q) for q in queries])
+    assert np.array_equal(lib.scores(queries), ref)
+    out = np.empty((64, 32), dtype=np.uint8)
+    for t in (0, 31, 100, 130, 191):
+        _lib.check(lib._lib.rs_vt_read(lib._h, t, _lib.ptr(out, ctypes.c_uint8)))
+        assert np.array_equal(out, lib_np[t]), t
+
+
 def test_small_batches_in_place_and_back_to_back_adds(vtmod):
     """Batches of at most 64 queries are read by the plane kernel straight from the
     pinned staging array (which also leaves their bytes on the device for the template

@@ -19,7 +19,7 @@ open('abtmp/%s.hip' % name, 'w').write(s)
 PY
 H=/opt/rocm/bin/hipcc
 $H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -Iinclude -Ipyratslam_amd/csrc -x hip \
-   -fno-slp-vectorize -c abtmp/$name.hip -o tools/ab/$name.pc.o
+   -fno-slp-vectorize -mllvm -amdgpu-kernarg-preload-count=9 -c abtmp/$name.hip -o tools/ab/$name.pc.o
 $H --offload-arch=gfx950 -shared -fPIC -o abtmp/$name.so pyratslam_amd/build/rs_common.o \
    tools/ab/$name.pc.o pyratslam_amd/build/view_templates.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo abtmp/$name.so

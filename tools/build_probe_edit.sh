@@ -17,5 +17,5 @@ for e in edits:
 open('abtmp/%s/posecell.hip' % name, 'w').write(s)
 PY
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Iabtmp/$name -Ipyratslam_amd/csrc -x hip \
-   -fno-slp-vectorize tools/pc_probe.hip pyratslam_amd/csrc/rs_common.cpp -o abtmp/${name}_probe
+   -fno-slp-vectorize -mllvm -amdgpu-kernarg-preload-count=9 tools/pc_probe.hip pyratslam_amd/csrc/rs_common.cpp -o abtmp/${name}_probe
 echo abtmp/${name}_probe

@@ -3,7 +3,7 @@
 // stamps (100 MHz) at their phase boundaries, then reports per-phase times
 // over the blocks of one step, and back-to-back launch costs of each kernel
 // alone and of an empty kernel with the same grid.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-kernarg-preload-count=7 -Iinclude -Ipyratslam_amd/csrc \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-kernarg-preload-count=9 -Iinclude -Ipyratslam_amd/csrc \
 //         tools/pc_probe.hip pyratslam_amd/csrc/rs_common.cpp -o /tmp/pc_probe
 #include <hip/hip_runtime.h>
 
@@ -194,6 +194,12 @@ int main(int argc, char** argv) {
             printf("   halo phase 1 (wave 0): LDS-DMA issued after %.2f us, landed after %.2f us (median)\n",
                    median(i1) * 1e-3, median(w1) * 1e-3);
         }
+        if (stamped(11, 2)) {   // the two-group image (round 6): wave 0's segment A, to the group-B wait
+            std::vector<double> sa;
+            for (int bb = 0; bb < h->nPart; ++bb)
+                sa.push_back((double)(st[((size_t)11 * 4096 + bb) * 8 + 2] - st[((size_t)7 * 4096 + bb) * 8 + 1]) * 10.0);
+            printf("   halo phase 2 (wave 0): group-A barrier -> segment A done %.2f us (median)\n", median(sa) * 1e-3);
+        }
         printf("   halo phase 2 per wave, task loop end after phase 1 (median us):");
         for (int w = 0; w < 9; ++w) {
             std::vector<double> c;
@@ -225,9 +231,9 @@ int main(int argc, char** argv) {
         make_ctl_halo(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, X, Y, h->cgx,
-                               (int)g.x, hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), (float*)h->dQ,
-                               h->dPart, h->nPart, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
+            hipLaunchKernelGGL((pc_step_halo<false>), g, b, 0, h->stream, (const float*)h->dP, hf_pack(X, Y),
+                               hf_pack(h->cgx, g.x), hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), hf_magic(h->cgx),
+                               hf_magic(c.uh), h->dPart, h->nPart, (float*)h->dQ, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
                                (const float*)h->dFilt, h->nf, c, h->kf, nullptr);
         CK(hipEventRecord(c1, h->stream));
         CK(hipEventSynchronize(c1));
