@@ -63,6 +63,7 @@ template <>
 struct PcNorm<float> {
     float r, t;
     bool div;
+    __device__ PcNorm(float r_, float t_, bool div_) : r(r_), t(t_), div(div_) {}
     __device__ explicit PcNorm(double tot) {
         const float rf = (float)(tot != 0.0 ? 1.0 / tot : 1.0);
         // wave-uniform (every lane formed the same total): a scalar branch below, so the
@@ -1356,8 +1357,18 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     const int tile = st_tile(blockIdx.x, nblk), xy = tile % (gx * gy);
     const int x0 = (xy % gx) * TX, y0 = (xy / gx) * TY;
     const CoLayers<CHUNK> ly = co_layers<CHUNK>(tile / (gx * gy), KC, TH);
+    // the fixed-extent instance's layer count is compile-time (no division per task)
+    const int nlc = FIX_TH > 0 ? FIX_TH : ly.nl;
     if (res_slot != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += blockDim.x) st_wt(&res_slot[i], 0ull);  // this step's path kernel max-reduces into them
+    // the taps and constants in scalar registers for the whole kernel (float32): hipcc
+    // otherwise reloads them from the kernel arguments after each barrier, a scalar
+    // round trip at the head of the x and theta passes
+    if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int q = 0; q < FL; ++q) asm volatile("" : "+s"(k.ge[q]), "+s"(k.gi[q]));
+        asm volatile("" : "+s"(k.scale), "+s"(k.inhib));
+    }
     PC_STAMP(5, 0);
     // y pass straight from the loads.  P is theta-fastest on this form (cell (x, y)
     // holds its TH layers contiguously), so task (r, L) = window row r of layer L
@@ -1434,8 +1445,8 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // one contiguous aligned run with no extra pass.
     T* s_xe = s_in;
     T* s_xi = s_in + TX * TY * PP;
-    for (int t = tid; t < ly.nl * TY; t += NT) {
-        const int c = t / ly.nl, L = t - c * ly.nl;
+    for (int t = tid; t < nlc * TY; t += NT) {
+        const int c = t / nlc, L = t - c * nlc;
         T ye[HX], yi[HX];
 #pragma unroll
         for (int a = 0; a < HX; ++a) {
@@ -1443,7 +1454,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
             yi[a] = s_yi[(a * TY + c) * THM + L];
         }
         // wrapped copies (TH >= 10, so at most one of each)
-        const int Lw1 = !CHUNK && L < 8 ? ly.nl + L : INT_MIN, Lw2 = !CHUNK && L >= ly.nl - 4 ? L - ly.nl : INT_MIN;
+        const int Lw1 = !CHUNK && L < 8 ? nlc + L : INT_MIN, Lw2 = !CHUNK && L >= nlc - 4 ? L - nlc : INT_MIN;
 #pragma unroll
         for (int i = 0; i < TX; ++i) {
             T e = 0, g = 0;
@@ -1473,7 +1484,7 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // then loads whole runs of each cell's layers)
     double sum = 0.0;
     {
-        const int ng = (ly.nout + VEC - 1) / VEC;
+        const int ng = FIX_TH > 0 ? FIX_TH / VEC : (ly.nout + VEC - 1) / VEC;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
         constexpr int ROFF = CHUNK ? 0 : 1, NRV = (ROFF + VEC + 2 * HALF + VEC - 1) / VEC;
@@ -1617,16 +1628,26 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     constexpr int WYP = TY + 2 * HALF + 6, LPC = DMA ? DMA_TH : (THM | 1), WXP = WBUF / (WYP * LPC);
     static_assert(WXP >= TX + 2 * HALF, "a per-layer window fits");
     bool dma = false;
+    // the union's fields (DMA instance) in scalar registers for the whole kernel: hipcc
+    // otherwise reloads them from the kernel arguments after the first barrier
+    int cumx = 0, cumy = 0, cuwx = 0, cuwy = 0;
+    if constexpr (DMA) {
+        cumx = __builtin_amdgcn_readfirstlane((int)ctl.umx);
+        cumy = __builtin_amdgcn_readfirstlane((int)ctl.umy);
+        cuwx = __builtin_amdgcn_readfirstlane((int)ctl.uwx);
+        cuwy = __builtin_amdgcn_readfirstlane((int)ctl.uwy);
+        asm volatile("" : "+s"(cumx), "+s"(cumy), "+s"(cuwx), "+s"(cuwy));
+    }
     if constexpr (DMA) {
         static_assert(sizeof(T) == 4 && !CHUNK && DMA_TH % 4 == 0 && DMA_TH <= THM, "DMA window form");
         constexpr int PPC = DMA_TH / 4;    // 16-byte pieces per cell
         static_assert(WXP * WYP * PPC + 63 <= WBUF / 4, "the last wave-instruction stays in the buffer");
-        const int WX = ctl.uwx, WY = ctl.uwy;
+        const int WX = cuwx, WY = cuwy;
         dma = TH == DMA_TH && WX <= WXP && WY <= WYP && WX <= X && WY <= Y;
         if (dma) {
             // piece p = (u * WYP + v) * PPC + l4 lands at s_w + 4p (the padding cells
             // v >= WY are not loaded); a thread's pieces advance by NT per instruction
-            const int ux0 = co_wrap(x0 - HALF + ctl.umx, X), uy0 = co_wrap(y0 - HALF + ctl.umy, Y);
+            const int ux0 = co_wrap(x0 - HALF + cumx, X), uy0 = co_wrap(y0 - HALF + cumy, Y);
             const int npc = WX * WYP * PPC, wave_u = __builtin_amdgcn_readfirstlane(wave);
             constexpr int DC = NT / PPC, DL = NT % PPC, DU = DC / WYP, DV = DC % WYP;
             constexpr int NK = (WXP * WYP * PPC + NT - 1) / NT;
@@ -1685,13 +1706,20 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // the normalisation total (every wave forms it itself) and the filter table into
     // LDS before the first barrier, which waits for the control's loads anyway: the
     // window's loads then follow with nothing else to wait for
-    double tot = 0.0;
+    // (the DMA instance forms it after the first barrier, in its last wave, which has no
+    // filter task: the partials are the youngest loads of every wave, so forming the total
+    // here waits for the whole window, and the DPP reduction and reciprocal sat between the
+    // window's landing and the barrier)
+    auto total = [&]() __attribute__((always_inline)) {
+        double tot = 0.0;
 #pragma unroll
-    for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
-    for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
-    tot = co_wave_sum(tot);
+        for (int u = 0; u < NPL; ++u) tot += lane + 64 * u < npart ? pt[u] : 0.0;
+        for (int i = lane + 64 * NPL; i < npart; i += 64) tot += part[i];
+        return co_wave_sum(tot);
+    };
     // the normalisation (:343-345): PcNorm (float32: the product with the reciprocal)
-    const PcNorm<T> nrm(tot);
+    __shared__ float s_nrm[3];   // (the DMA instance: r, t, div of the total's PcNorm<float>)
+    const PcNorm<T> nrm0(DMA ? 1.0 : total());
 #pragma unroll
     for (int u = 0; u < NFR; ++u) {
         const int i = tid + u * NT, fi = i / FT;
@@ -1707,10 +1735,10 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     int mnx = INT_MAX, mxx = INT_MIN, mny = INT_MAX, mxy = INT_MIN;
     if (DMA && dma) {
         if constexpr (DMA) {
-            mnx = ctl.umx;
-            mny = ctl.umy;
-            mxx = mnx + ctl.uwx - (TX + 2 * HALF);
-            mxy = mny + ctl.uwy - (TY + 2 * HALF);
+            mnx = cumx;
+            mny = cumy;
+            mxx = mnx + cuwx - (TX + 2 * HALF);
+            mxy = mny + cuwy - (TY + 2 * HALF);
         }
     } else {
         for (int L = lane; L < ly.nl; L += 64) {
@@ -1730,7 +1758,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
 
     constexpr int FS = CO_FSPLIT, TXH = TX / FS, CP = CO_FCOLS, NCG = TY / CP;
     static_assert(TX % FS == 0 && TY % CP == 0, "filter task shape");
-    const int nl = ly.nl;
+    const int nl = DMA ? DMA_TH : ly.nl;   // (the DMA instance runs at TH == DMA_TH only: no division per task)
     if (DMA && dma) {
         // the window is in LDS already
     } else if (uni && !CHUNK && TH % VEC == 0) {
@@ -1814,6 +1842,17 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     }
     if (!(DMA && dma)) co_lds_barrier();
     PC_STAMP(6, 2);
+    if constexpr (DMA) {
+        static_assert(DMA_TH * NCG * FS <= 64 * (NW - 1), "the last wave has no filter task");
+        if (wave == NW - 1) {
+            const PcNorm<float> n1(total());
+            if (lane == 0) {
+                s_nrm[0] = n1.r;
+                s_nrm[1] = n1.t;
+                s_nrm[2] = n1.div ? 1.f : 0.f;
+            }
+        }
+    }
     // 7x7 filter: task (layer, column group, row part) -> TX/FS rows x CP columns of
     // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each window
     // row's reads; reads of CO_FROWS rows at a time in flight: hoisting all of them
@@ -1877,6 +1916,9 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     (void)VEC;
     co_lds_barrier();
     PC_STAMP(6, 3);
+    PcNorm<T> nrm = nrm0;
+    if constexpr (DMA)   // (div block-uniform: a scalar branch)
+        nrm = PcNorm<T>(s_nrm[0], s_nrm[1], __builtin_amdgcn_readfirstlane((int)(s_nrm[2] != 0.f)) != 0);
     // theta pass, clamp, normalisation, argmax: task (cell p, chunk j).  float32:
     // the first maximum as the largest packed (value, ~index) key; float64: value
     // and index pairs
@@ -1888,7 +1930,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         // of one cell: P is theta-fastest on this form, so a group is one 16-byte
         // store and a wave's stores cover consecutive cells' theta columns
         using V = typename CoVec<T>::type;
-        const int ng = (ly.nout + VEC - 1) / VEC;
+        const int ng = DMA ? DMA_TH / VEC : (ly.nout + VEC - 1) / VEC;
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(T), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(T) <= (size_t)INT_MAX;
 #pragma unroll 1
@@ -2022,7 +2064,8 @@ constexpr int HF_UMAX = 22 * 22;              // union cells staged by LDS-DMA (
 // theta-pass windows, (e, i) pairs [j][rx][ry], row pitch 18 pairs: the y pass's 16-byte
 // row reads (16 lanes on consecutive rows, 36 dwords apart) are conflict-free
 constexpr int HF_WP = 18, HF_WJ = HF_W * HF_WP;
-constexpr int HF_YJ = HF_W * HF_Q + 10;       // y-pass outputs per layer (pitch: the x pass reads conflict-free)
+constexpr int HF_YC = HF_W + 4;               // y-pass outputs per Q column (16 rows, 16-byte aligned)
+constexpr int HF_YL = HF_Q * HF_YC;           // ... per layer, [qc][rx]
 constexpr int HF_QJ = HF_Q * HF_Q + 4;        // Q window per layer
 constexpr int HF_EXP_MAX = 64;                // steps whose keys pc_halo_finish exports itself
 constexpr float HF_NEAR = 0x1p-20f;           // relative margin of a possible rounding tie (pc_halo_export)
@@ -2097,7 +2140,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     constexpr int TH = HF_TH, NV = TH / 4;   // 16-byte pieces per theta column
     static_assert(TH % 4 == 0, "theta columns of whole 16-byte pieces");
     constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
-    constexpr int YBUF = 2 * TH * HF_YJ;
+    constexpr int YBUF = 2 * TH * HF_YL;
     constexpr int BBUF = WBUF > YBUF ? WBUF : YBUF;
     constexpr int PP = TH + 64;   // path outputs per cell: rows TH dwords apart modulo the 64 banks
     static_assert(HF_T * HF_T * PP <= BBUF && TH * HF_QJ <= 2 * TH * HF_WJ, "buffer reuse");
@@ -2187,6 +2230,14 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     }
     int cwrap = ctl.wrap;
     asm volatile("" : "+s"(cwrap));
+    // likewise the inhibition's constants (phase 4) and the theta filter (phase 6)
+    float kscale = k.scale, kinhib = k.inhib, zf[FL];
+    asm volatile("" : "+s"(kscale), "+s"(kinhib));
+#pragma unroll
+    for (int z = 0; z < FL; ++z) {
+        zf[z] = ctl.zf[z];
+        asm volatile("" : "+s"(zf[z]));
+    }
     if (slot_zero != nullptr && blockIdx.x == 0)
         for (int i = tid; i < RES_SLOTS; i += HF_NT) st_wt(&slot_zero[i], 0ull);  // the next launch max-reduces into them
     if (dma) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's LDS-DMA pieces have landed
@@ -2397,9 +2448,12 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     co_lds_barrier();
     PC_STAMP(7, 2);
 
-    // 3. y pass: task (layer j, window row rx) -> 10 outputs of each Gaussian
+    // 3. y pass: task (layer j, window row rx) -> 10 outputs of each Gaussian, stored
+    //    transposed, [j][qc][rx] (column pitch HF_YC), so that the x pass reads each
+    //    column as four 16-byte vectors (conflict-free: lanes on consecutive columns are
+    //    20 dwords apart, layers HF_YL apart)
     float* s_ye = s_b;
-    float* s_yi = s_b + TH * HF_YJ;
+    float* s_yi = s_b + TH * HF_YL;
     for (int t = tid; t < TH * HF_W; t += HF_NT) {
         const int j = t >> 4, rx = t & 15;
         const co_f4* rw = reinterpret_cast<const co_f4*>(s_tw + j * HF_WJ + rx * HF_WP);
@@ -2410,20 +2464,15 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             w[2 * q] = hf_f2{a.x, a.y};
             w[2 * q + 1] = hf_f2{a.z, a.w};
         }
-        hf_f2* de = reinterpret_cast<hf_f2*>(s_ye + j * HF_YJ + rx * HF_Q);
-        hf_f2* di = reinterpret_cast<hf_f2*>(s_yi + j * HF_YJ + rx * HF_Q);
+        float* de = s_ye + j * HF_YL + rx;
+        float* di = s_yi + j * HF_YL + rx;
 #pragma unroll
-        for (int c2 = 0; c2 < HF_Q / 2; ++c2) {
-            hf_f2 o[2];
+        for (int qc = 0; qc < HF_Q; ++qc) {
+            hf_f2 eg = {0.f, 0.f};
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                hf_f2 eg = {0.f, 0.f};
-#pragma unroll
-                for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[2 * c2 + h + t2];
-                o[h] = eg;
-            }
-            de[c2] = hf_f2{o[0].x, o[1].x};
-            di[c2] = hf_f2{o[0].y, o[1].y};
+            for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[qc + t2];
+            de[qc * HF_YC] = eg.x;
+            di[qc * HF_YC] = eg.y;
         }
     }
     co_lds_barrier();
@@ -2435,19 +2484,23 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     double qs = 0.0;
     for (int t = tid; t < TH * HF_Q; t += HF_NT) {
         const int j = t / HF_Q, qc = t - j * HF_Q;
-        const float* ce = s_ye + j * HF_YJ + qc;
-        const float* ci = s_yi + j * HF_YJ + qc;
+        const co_f4* ce = reinterpret_cast<const co_f4*>(s_ye + j * HF_YL + qc * HF_YC);
+        const co_f4* ci = reinterpret_cast<const co_f4*>(s_yi + j * HF_YL + qc * HF_YC);
         hf_f2 w[HF_W];
 #pragma unroll
-        for (int r = 0; r < HF_W; ++r) w[r] = hf_f2{ce[r * HF_Q], ci[r * HF_Q]};
+        for (int r4 = 0; r4 < HF_W / 4; ++r4) {
+            const co_f4 a = ce[r4], b = ci[r4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) w[4 * r4 + u] = hf_f2{a[u], b[u]};
+        }
         const bool ocol = (unsigned)(qc - HALF) < (unsigned)tht;
 #pragma unroll
         for (int qa = 0; qa < HF_Q; ++qa) {
             hf_f2 eg = {0.f, 0.f};
 #pragma unroll
             for (int a = 0; a < FL; ++a) eg += gei[a] * w[qa + a];
-            const float v = (eg.x - eg.y) * k.scale;
-            const float q = (v < k.inhib) ? 0.f : v - k.inhib;
+            const float v = (eg.x - eg.y) * kscale;
+            const float q = (v < kinhib) ? 0.f : v - kinhib;
             const bool own = ocol && (unsigned)(qa - HALF) < (unsigned)tw;
             if (own) qs += (double)q;
             if constexpr (EXC) {
@@ -2526,7 +2579,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             for (int o = 0; o < 4; ++o) {
                 float x = 0.f;
 #pragma unroll
-                for (int z = 0; z < FL; ++z) x += r[o + z] * ctl.zf[z];
+                for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
                 v[o] = pc_clamp(x);
             }
             const unsigned lin = ((unsigned)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g;
@@ -2540,6 +2593,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
         }
     }
+    PC_STAMP(14, 0);
     // the block's partial sum and argmax key
     qs = co_wave_sum(qs);
     if (lane == 0) s_red[wave] = qs;
@@ -2551,7 +2605,9 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         rk = co_wave_max(rk);
         if (lane == 0) s_rk[wave] = rk;
     }
+    PC_STAMP(14, 1);
     co_lds_barrier();
+    PC_STAMP(14, 2);
     if (rec) {
         // the block's record: its largest U's key and the count of its outputs within
         // HF_NEAR of that value (the maximum itself included)

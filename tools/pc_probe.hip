@@ -200,6 +200,18 @@ int main(int argc, char** argv) {
                 sa.push_back((double)(st[((size_t)11 * 4096 + bb) * 8 + 2] - st[((size_t)7 * 4096 + bb) * 8 + 1]) * 10.0);
             printf("   halo phase 2 (wave 0): group-A barrier -> segment A done %.2f us (median)\n", median(sa) * 1e-3);
         }
+        if (stamped(14, 0) && stamped(14, 1) && stamped(14, 2) && stamped(7, 5)) {   // phase 6's parts (wave 0)
+            std::vector<double> f, r, b;
+            for (int bb = 0; bb < h->nPart; ++bb) {
+                const unsigned long long* r13 = &st[((size_t)14 * 4096 + bb) * 8];
+                const unsigned long long p5 = st[((size_t)7 * 4096 + bb) * 8 + 5];
+                f.push_back((double)(r13[0] - p5) * 10.0);
+                r.push_back((double)(r13[1] - r13[0]) * 10.0);
+                b.push_back((double)(r13[2] - r13[1]) * 10.0);
+            }
+            printf("   halo phase 6 (wave 0): theta filter + store %.2f, reductions %.2f, barrier %.2f us (median)\n",
+                   median(f) * 1e-3, median(r) * 1e-3, median(b) * 1e-3);
+        }
         printf("   halo phase 2 per wave, task loop end after phase 1 (median us):");
         for (int w = 0; w < 9; ++w) {
             std::vector<double> c;
