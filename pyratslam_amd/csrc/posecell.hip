@@ -2151,7 +2151,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     __shared__ __attribute__((aligned(16))) float s_ftab[RT_NFMAX * ST_FTP];
     __shared__ int s_fo[TH];
     __shared__ double s_red[HF_NW];
-    __shared__ unsigned long long s_bk[HF_NW], s_rk[HF_NW];
+    __shared__ unsigned long long s_rk[HF_NW];
     __shared__ int s_cnt[HF_NW];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2518,9 +2518,36 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     unsigned long long rk = 0ull;
     co_f4 uv = {0.f, 0.f, 0.f, 0.f};
     bool has_uv = false;
+    // every thread's partial sum and key, past Q in s_t (free from here on): the last
+    // wave, which has no task in phase 5, reduces them there -- lane l adds the values of
+    // thread l of every wave in wave order, then one DPP reduction (a fixed order, so
+    // every launch gives the same bits) -- and stores the block's partial sum and key, so
+    // the block's tail is the theta filter and its store
+    constexpr int QSW = (TH * HF_QJ + 1) / 2 * 2;   // (8-byte aligned)
+    double* s_qsw = reinterpret_cast<double*>(s_t + QSW);
+    unsigned long long* s_bkw = reinterpret_cast<unsigned long long*>(s_qsw + HF_NT);
+    static_assert(QSW + 4 * HF_NT <= 2 * (TH * HF_WJ + HF_NT), "per-thread sums and keys in s_t");
     if constexpr (!EXC) {
+        s_qsw[tid] = qs;
+        s_bkw[tid] = bk;
         co_lds_barrier();
         PC_STAMP(7, 4);
+        static_assert(TH * 8 <= (HF_NW - 1) * 64, "the last wave has no phase-5 task");
+        if (wave == HF_NW - 1) {
+            double v = 0.0;
+            unsigned long long kb = 0ull;
+#pragma unroll
+            for (int w = 0; w < HF_NW; ++w) {
+                v += s_qsw[w * 64 + lane];
+                kb = max(kb, s_bkw[w * 64 + lane]);
+            }
+            const double bsum = co_wave_sum(v);
+            if (want_key) kb = co_wave_max(kb);
+            if (lane == 0) {
+                st_wt(&part_out[blockIdx.x], bsum);
+                if (want_key) atomicMax(slot_prev + (blockIdx.x & (RES_SLOTS - 1)), kb);
+            }
+        }
         // 5. 7 x 7 path filter (:273) + clamp (:300): task (layer j, tile column tb,
         //    row pair ap) -> 2 outputs from 8 x 7 Q values; into [cell][3 + j] rows with
         //    wrapped copies (layers TH-3.. before, 0..6 after), so every theta window
@@ -2594,19 +2621,23 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     }
     PC_STAMP(14, 0);
-    // the block's partial sum and argmax key
-    qs = co_wave_sum(qs);
-    if (lane == 0) s_red[wave] = qs;
-    if (want_key) {
-        bk = co_wave_max(bk);
-        if (lane == 0) s_bk[wave] = bk;
+    if constexpr (EXC) {   // (the excitation-only instance: the block's partial sum at its end)
+        qs = co_wave_sum(qs);
+        if (lane == 0) s_red[wave] = qs;
+        co_lds_barrier();
+        if (tid == 0) {
+            double bsum = 0.0;
+#pragma unroll
+            for (int w = 0; w < HF_NW; ++w) bsum += s_red[w];
+            st_wt(&part_out[blockIdx.x], bsum);
+        }
     }
     if (rec) {
         rk = co_wave_max(rk);
         if (lane == 0) s_rk[wave] = rk;
+        co_lds_barrier();
     }
     PC_STAMP(14, 1);
-    co_lds_barrier();
     PC_STAMP(14, 2);
     if (rec) {
         // the block's record: its largest U's key and the count of its outputs within
@@ -2632,16 +2663,6 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             // 16.8-18.9 us, tools/pc_ab.py --mode update, round 5.)
             typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
             *reinterpret_cast<u2*>(rec + 2 * blockIdx.x) = u2{m, REC_SET | (unsigned long long)cnt};
-        }
-    }
-    if (tid == 0) {
-        double bsum = 0.0;
-#pragma unroll
-        for (int w = 0; w < HF_NW; ++w) bsum += s_red[w];
-        st_wt(&part_out[blockIdx.x], bsum);
-        if (want_key) {
-            for (int w = 1; w < HF_NW; ++w) bk = max(bk, s_bk[w]);
-            atomicMax(slot_prev + (blockIdx.x & (RES_SLOTS - 1)), bk);
         }
     }
     PC_STAMP(7, 6);

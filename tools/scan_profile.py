@@ -89,7 +89,11 @@ def main():
     p.add_argument('--steps', type=int, default=400)
     for x in (s, p):
         x.add_argument('--clock-warmup-ms', type=float, default=200.0)
+        x.add_argument('--lib', default=None, help='a library build to load instead of the in-tree one (A/B)')
     a = ap.parse_args()
+    if a.lib:
+        from pyratslam_amd import _lib
+        _lib.load(a.lib)
     scan(a) if a.what == 'scan' else pc(a)
 
 

@@ -4,6 +4,7 @@ batches of 1,024 queries against 1,000 templates) across library builds, each in
 its own process, interleaved over rounds (GPU box).
 usage: python tools/stream_ab.py LIB.so [LIB2.so ...] [--rounds 3] [--steps 60]"""
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -31,7 +32,10 @@ def child(path, steps):
     for _ in range(steps):
         vts.match_stream((10, 1024, buf))
     dt = (time.perf_counter() - t0) / steps
-    print(json.dumps({'lib': path, 'ms_per_step': 1e3 * dt, 'gcompares_per_s': 10240 * 1000 / dt / 1e9}))
+    idx, score = vts.match_stream((10, 1024, buf))
+    h = hashlib.sha256(np.ascontiguousarray(idx).tobytes() + np.ascontiguousarray(score).tobytes()).hexdigest()[:16]
+    print(json.dumps({'lib': path, 'ms_per_step': 1e3 * dt, 'gcompares_per_s': 10240 * 1000 / dt / 1e9,
+                      'keys_sha16': h}))
 
 
 def main():
@@ -45,6 +49,7 @@ def main():
         child(a.libs[0], a.steps)
         return
     res = {l: [] for l in a.libs}
+    keys, bad = {}, False
     for _ in range(a.rounds):
         for lib in a.libs:
             p = subprocess.run([sys.executable, __file__, lib, '--child', '--steps', str(a.steps)],
@@ -52,10 +57,18 @@ def main():
             if p.returncode != 0:
                 print(p.stderr[-2000:], file=sys.stderr)
                 raise SystemExit(p.returncode)
-            res[lib].append(json.loads(p.stdout.strip().splitlines()[-1])['ms_per_step'])
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            res[lib].append(r['ms_per_step'])
+            keys.setdefault(lib, r['keys_sha16'])
+            if r['keys_sha16'] != keys[a.libs[0]]:
+                print('stream_ab: INVALID A/B -- %s returns other keys than %s' % (lib, a.libs[0]), file=sys.stderr)
+                bad = True
     for lib in a.libs:
         v = sorted(res[lib])
-        print(json.dumps({'lib': lib, 'ms_per_step_median': v[len(v) // 2], 'all': [round(x, 4) for x in res[lib]]}))
+        print(json.dumps({'lib': lib, 'ms_per_step_median': v[len(v) // 2], 'all': [round(x, 4) for x in res[lib]],
+                          'keys_sha16': keys[lib]}))
+    if bad:
+        raise SystemExit(1)
 
 
 if __name__ == '__main__':
