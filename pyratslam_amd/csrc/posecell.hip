@@ -1445,25 +1445,26 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // one contiguous aligned run with no extra pass.
     T* s_xe = s_in;
     T* s_xi = s_in + TX * TY * PP;
-    for (int t = tid; t < nlc * TY; t += NT) {
-        const int c = t / nlc, L = t - c * nlc;
-        T ye[HX], yi[HX];
+    // one task: outputs i0 .. i0 + R - 1 of column c, layer L
+    auto xtask = [&](int c, int L, int i0, auto r_c) __attribute__((always_inline)) {
+        constexpr int R = decltype(r_c)::value;
+        T ye[R + 2 * HALF], yi[R + 2 * HALF];
 #pragma unroll
-        for (int a = 0; a < HX; ++a) {
-            ye[a] = s_ye[(a * TY + c) * THM + L];
-            yi[a] = s_yi[(a * TY + c) * THM + L];
+        for (int a = 0; a < R + 2 * HALF; ++a) {
+            ye[a] = s_ye[((i0 + a) * TY + c) * THM + L];
+            yi[a] = s_yi[((i0 + a) * TY + c) * THM + L];
         }
         // wrapped copies (TH >= 10, so at most one of each)
         const int Lw1 = !CHUNK && L < 8 ? nlc + L : INT_MIN, Lw2 = !CHUNK && L >= nlc - 4 ? L - nlc : INT_MIN;
 #pragma unroll
-        for (int i = 0; i < TX; ++i) {
+        for (int i = 0; i < R; ++i) {
             T e = 0, g = 0;
 #pragma unroll
             for (int q = 0; q < FL; ++q) {
                 e += k.ge[q] * ye[i + q];
                 g += k.gi[q] * yi[i + q];
             }
-            const int r = (i * TY + c) * PP + SPO;
+            const int r = ((i0 + i) * TY + c) * PP + SPO;
             s_xe[r + L] = e;
             s_xi[r + L] = g;
             if (Lw1 != INT_MIN) {
@@ -1474,6 +1475,20 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
                 s_xe[r + Lw2] = e;
                 s_xi[r + Lw2] = g;
             }
+        }
+    };
+    if constexpr (FIX_TH == 72 && TX == 8 && TY == 8 && NW == 12) {
+        // the 72-layer instance balances the four SIMDs (wave w runs on SIMD w % 4):
+        // waves 0-7 take layers 0-63 (lane = layer) of column w, waves 8-11 layers 64-71
+        // (64 + (lane & 7)) of column lane >> 3, two of the eight outputs each; 576 equal
+        // tasks on 9 waves put three on SIMD 0
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+        if (wave < 8) xtask(wave, lane, 0, std::integral_constant<int, TX>{});
+        else xtask(lane >> 3, 64 + (lane & 7), 2 * (wave - 8), std::integral_constant<int, 2>{});
+    } else {
+        for (int t = tid; t < nlc * TY; t += NT) {
+            const int c = t / nlc, L = t - c * nlc;
+            xtask(c, L, 0, std::integral_constant<int, TX>{});
         }
     }
     co_lds_barrier();
@@ -1857,26 +1872,27 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
     // outputs from TX/FS + 6 window rows of CP + 6 cells (CP columns share each window
     // row's reads; reads of CO_FROWS rows at a time in flight: hoisting all of them
     // spills at 3 waves per SIMD).  Layer fastest over the lanes.
-    for (int t = tid; t < nl * NCG * FS; t += NT) {
-        const int L = t % nl, rem = t / nl, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
+    // one task: R output rows from tile row x0r, CP columns from c0, of layer L
+    auto ftask = [&](int L, int x0r, int c0, auto r_c) __attribute__((always_inline)) {
+        constexpr int R = decltype(r_c)::value;
         T f[FT];
         st_filter<T>(s_ftab + s_fo[L], f);
-        T acc[TXH][CP];
+        T acc[R][CP];
 #pragma unroll
-        for (int i = 0; i < TXH; ++i)
+        for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int c = 0; c < CP; ++c) acc[i][c] = 0;
         const int dx = uni ? s_ox[L] - mnx : 0, dy = uni ? s_oy[L] - mny : 0;
         // the base index is opaque to the compiler, so each read keeps its compile-time
         // offset as an immediate (ds_read2_b32 pairs) instead of an address add each
-        int wbase = ((hf * TXH + dx) * WYP + c0 + dy) * LPC + L;
+        int wbase = ((x0r + dx) * WYP + c0 + dy) * LPC + L;
         asm volatile("" : "+v"(wbase));
         const T* win = s_w + wbase;
         // the window rows in a rotated order per wave group (waves w, w+4, w+8 share a
         // SIMD): the groups' LDS read bursts and FMA runs interleave instead of
         // running in lockstep behind the barrier
         auto rows = [&](auto rot_c) __attribute__((always_inline)) {
-            constexpr int ROT = decltype(rot_c)::value, NRW = TXH + 2 * HALF;
+            constexpr int ROT = decltype(rot_c)::value, NRW = R + 2 * HALF;
 #pragma unroll
             for (int aa = 0; aa < NRW; ++aa) {
                 const int a = (aa + ROT) % NRW;
@@ -1885,7 +1901,7 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
                 for (int q = 0; q < FL + CP - 1; ++q) w[q] = win[(a * WYP + q) * LPC];
                 if (aa % CO_FROWS == CO_FROWS - 1) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int i = 0; i < TXH; ++i) {
+                for (int i = 0; i < R; ++i) {
                     const int x = a - i;
                     if (x < 0 || x >= FL) continue;
 #pragma unroll
@@ -1903,15 +1919,30 @@ __global__ __launch_bounds__(64 * NW) void pc_path_cols(
         // before SPO, 0..7 also after SPO + TH; TH >= 10, so at most one of each)
         const int Lw1 = !CHUNK && L < 8 ? nl + L : INT_MIN, Lw2 = !CHUNK && L >= nl - 4 ? L - nl : INT_MIN;
 #pragma unroll
-        for (int i = 0; i < TXH; ++i)
+        for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int c = 0; c < CP; ++c) {
                 const T v = pc_clamp(acc[i][c]);
-                T* sp = s_p + ((hf * TXH + i) * TY + c0 + c) * PP + SPO;
+                T* sp = s_p + ((x0r + i) * TY + c0 + c) * PP + SPO;
                 sp[L] = v;
                 if (Lw1 != INT_MIN) sp[Lw1] = v;
                 if (Lw2 != INT_MIN) sp[Lw2] = v;
             }
+    };
+    if constexpr (DMA) {
+        // The DMA instance (72 layers, 8 x 8 tiles, 12 waves) balances the four SIMDs
+        // (wave w runs on SIMD w % 4): waves 0-7 take layers 0-63 (lane = layer) in
+        // 4-row x 2-column tasks, waves 8-11 layers 64-71 in 1-row x 2-column tasks
+        // (layer 64 + (lane & 7), tile row lane >> 3).  Every SIMD issues 2 x 392 + 98
+        // filter FMAs per lane, where 576 equal tasks on 9 waves put 3 x 392 on SIMD 0
+        static_assert(TX == 8 && TY == 8 && CP == 2 && FS == 2 && NW == 12 && DMA_TH == 72, "DMA instance's task split");
+        if (wave < 8) ftask(lane, (wave >> 2) * TXH, (wave & 3) * CP, std::integral_constant<int, TXH>{});
+        else ftask(64 + (lane & 7), lane >> 3, (wave - 8) * CP, std::integral_constant<int, 1>{});
+    } else {
+        for (int t = tid; t < nl * NCG * FS; t += NT) {
+            const int L = t % nl, rem = t / nl, hf = rem / NCG, c0 = (rem - hf * NCG) * CP;
+            ftask(L, hf * TXH, c0, std::integral_constant<int, TXH>{});
+        }
     }
     (void)VEC;
     co_lds_barrier();
@@ -2454,12 +2485,15 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     //    20 dwords apart, layers HF_YL apart)
     float* s_ye = s_b;
     float* s_yi = s_b + TH * HF_YL;
-    for (int t = tid; t < TH * HF_W; t += HF_NT) {
-        const int j = t >> 4, rx = t & 15;
+    // task (layer j, row rx, outputs QC0 .. QC0 + NQ - 1); the SIMDs are balanced (wave w
+    // runs on SIMD w % 4): waves 0-7 take layers 0-31 whole, one wave per SIMD (8, 5, 6, 7)
+    // a part of layers 32-35 (576 whole tasks on 9 waves put three on SIMD 0)
+    auto ytask = [&](int j, int rx, auto qc0_c, auto nq_c) __attribute__((always_inline)) {
+        constexpr int QC0 = decltype(qc0_c)::value, NQ = decltype(nq_c)::value;
         const co_f4* rw = reinterpret_cast<const co_f4*>(s_tw + j * HF_WJ + rx * HF_WP);
-        hf_f2 w[HF_W];   // (e, i) of the row's 16 cells
+        hf_f2 w[HF_W];   // (e, i) of the row's 16 cells (those the outputs reach)
 #pragma unroll
-        for (int q = 0; q < HF_W / 2; ++q) {
+        for (int q = QC0 / 2; q <= (QC0 + NQ + 2 * HALF - 1) / 2; ++q) {
             const co_f4 a = rw[q];
             w[2 * q] = hf_f2{a.x, a.y};
             w[2 * q + 1] = hf_f2{a.z, a.w};
@@ -2467,13 +2501,23 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         float* de = s_ye + j * HF_YL + rx;
         float* di = s_yi + j * HF_YL + rx;
 #pragma unroll
-        for (int qc = 0; qc < HF_Q; ++qc) {
+        for (int qc = QC0; qc < QC0 + NQ; ++qc) {
             hf_f2 eg = {0.f, 0.f};
 #pragma unroll
             for (int t2 = 0; t2 < FL; ++t2) eg += gei[t2] * w[qc + t2];
             de[qc * HF_YC] = eg.x;
             di[qc * HF_YC] = eg.y;
         }
+    };
+    static_assert(TH == 36 && HF_W == 16 && HF_Q == 10 && HF_NW == 9, "phase 3's task split");
+    {
+        using I = std::integral_constant<int, 0>;
+        if (wave < 8) ytask(tid >> 4, tid & 15, I{}, std::integral_constant<int, HF_Q>{});
+        const int jr = 32 + (lane >> 4), rr = lane & 15;
+        if (wave == 8) ytask(jr, rr, I{}, std::integral_constant<int, 3>{});
+        else if (wave == 5) ytask(jr, rr, std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+        else if (wave == 6) ytask(jr, rr, std::integral_constant<int, 6>{}, std::integral_constant<int, 2>{});
+        else if (wave == 7) ytask(jr, rr, std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{});
     }
     co_lds_barrier();
     PC_STAMP(7, 3);
@@ -2482,23 +2526,29 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     //    the partial sum over the layer's shifted own tile (Q rows/columns 3 .. 3+tw)
     float* s_q = s_t;
     double qs = 0.0;
-    for (int t = tid; t < TH * HF_Q; t += HF_NT) {
+    // task (layer j, Q column qc, Q rows 5H .. 5H + 4), H-uniform per wave; the SIMDs are
+    // balanced: H = 0 on waves 0-5, H = 1 on waves 8, 6, 7, 1, 2, 3 (three 5-row tasks
+    // per SIMD, where 360 10-row tasks on 6 waves put two on SIMDs 0 and 1)
+    auto xtask = [&](int t, auto h_c) __attribute__((always_inline)) {
+        constexpr int H = decltype(h_c)::value;
+        if (t >= TH * HF_Q) return;
         const int j = t / HF_Q, qc = t - j * HF_Q;
-        const co_f4* ce = reinterpret_cast<const co_f4*>(s_ye + j * HF_YL + qc * HF_YC);
-        const co_f4* ci = reinterpret_cast<const co_f4*>(s_yi + j * HF_YL + qc * HF_YC);
-        hf_f2 w[HF_W];
+        const co_f4* ce = reinterpret_cast<const co_f4*>(s_ye + j * HF_YL + qc * HF_YC) + H;
+        const co_f4* ci = reinterpret_cast<const co_f4*>(s_yi + j * HF_YL + qc * HF_YC) + H;
+        hf_f2 w[12];   // rows 4H .. 4H + 11
 #pragma unroll
-        for (int r4 = 0; r4 < HF_W / 4; ++r4) {
+        for (int r4 = 0; r4 < 3; ++r4) {
             const co_f4 a = ce[r4], b = ci[r4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) w[4 * r4 + u] = hf_f2{a[u], b[u]};
         }
         const bool ocol = (unsigned)(qc - HALF) < (unsigned)tht;
 #pragma unroll
-        for (int qa = 0; qa < HF_Q; ++qa) {
+        for (int o = 0; o < 5; ++o) {
+            const int qa = 5 * H + o;
             hf_f2 eg = {0.f, 0.f};
 #pragma unroll
-            for (int a = 0; a < FL; ++a) eg += gei[a] * w[qa + a];
+            for (int a = 0; a < FL; ++a) eg += gei[a] * w[H + o + a];
             const float v = (eg.x - eg.y) * kscale;
             const float q = (v < kinhib) ? 0.f : v - kinhib;
             const bool own = ocol && (unsigned)(qa - HALF) < (unsigned)tw;
@@ -2509,6 +2559,12 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 s_q[j * HF_QJ + qa * HF_Q + qc] = q;
             }
         }
+    };
+    static_assert(TH * HF_Q <= 6 * 64 && TH * HF_Q > 5 * 64, "phase 4's task split: 6 wave-tasks per half");
+    if (wave < 6) xtask(wave * 64 + lane, std::integral_constant<int, 0>{});
+    {
+        const int s1 = wave == 8 ? 0 : wave == 6 ? 1 : wave == 7 ? 2 : wave == 1 ? 3 : wave == 2 ? 4 : wave == 3 ? 5 : -1;
+        if (s1 >= 0) xtask(s1 * 64 + lane, std::integral_constant<int, 1>{});
     }
     float* s_po = s_b;
     // rec (the last step of a call that leaves the state unnormalised, pc_run_halo):
@@ -2552,36 +2608,41 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         //    row pair ap) -> 2 outputs from 8 x 7 Q values; into [cell][3 + j] rows with
         //    wrapped copies (layers TH-3.. before, 0..6 after), so every theta window
         //    below is one contiguous aligned run
-        for (int t = tid; t < TH * 8; t += HF_NT) {
-            const int j = t >> 3, tb = t & 3, ap = (t >> 2) & 1;
+        //    The SIMDs are balanced: waves 0-3 take layers 0-31 (2-row tasks), wave 5 layers
+        //    32-35 as 1-row tasks (lane: layer 32 + (lane >> 4), row (lane >> 2) & 3, column
+        //    lane & 3); 288 2-row tasks on waves 0-4 put two on SIMD 0, beside wave 8
+        auto ptask = [&](int j, int tb, int a0, auto n_c) __attribute__((always_inline)) {
+            constexpr int NO = decltype(n_c)::value;
             float f[FT];
             st_filter<float>(s_ftab + s_fo[j], f);
-            float a0 = 0.f, a1 = 0.f;
-            const float* qw = s_q + j * HF_QJ + 2 * ap * HF_Q + tb;
+            float acc[NO];
 #pragma unroll
-            for (int r = 0; r < 2 + 2 * HALF; ++r) {  // rows of both outputs: 0..6 and 1..7
+            for (int h = 0; h < NO; ++h) acc[h] = 0.f;
+            const float* qw = s_q + j * HF_QJ + a0 * HF_Q + tb;
+#pragma unroll
+            for (int r = 0; r < NO + 2 * HALF; ++r) {  // rows of the outputs: h .. h + 6
                 float w[FL];
 #pragma unroll
                 for (int y = 0; y < FL; ++y) w[y] = qw[r * HF_Q + y];
-                if (r < FL) {
 #pragma unroll
-                    for (int y = 0; y < FL; ++y) a0 += w[y] * f[r * FL + y];
-                }
-                if (r >= 1) {
+                for (int h = 0; h < NO; ++h) {
+                    if (r - h < 0 || r - h >= FL) continue;
 #pragma unroll
-                    for (int y = 0; y < FL; ++y) a1 += w[y] * f[(r - 1) * FL + y];
+                    for (int y = 0; y < FL; ++y) acc[h] += w[y] * f[(r - h) * FL + y];
                 }
             }
-            const float v0 = pc_clamp(a0), v1 = pc_clamp(a1);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float v = h ? v1 : v0;
-                float* sp = s_po + ((2 * ap + h) * HF_T + tb) * PP;
+            for (int h = 0; h < NO; ++h) {
+                const float v = pc_clamp(acc[h]);
+                float* sp = s_po + ((a0 + h) * HF_T + tb) * PP;
                 sp[HALF + j] = v;
                 if (j >= TH - HALF) sp[j - TH + HALF] = v;
                 if (j < FL) sp[HALF + TH + j] = v;
             }
-        }
+        };
+        static_assert(TH == 36 && HF_T == 4, "phase 5's task split");
+        if (wave < 4) ptask(tid >> 3, tid & 3, 2 * ((tid >> 2) & 1), std::integral_constant<int, 2>{});
+        else if (wave == 5) ptask(32 + (lane >> 4), lane & 3, (lane >> 2) & 3, std::integral_constant<int, 1>{});
         co_lds_barrier();
         PC_STAMP(7, 5);
         // 6. theta filter (:310) + clamp (:314): task (cell, group of 4 layers) -> one
