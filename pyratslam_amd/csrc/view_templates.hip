@@ -1643,10 +1643,14 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
             if (h->timing) RS_HIP(hipEventRecord(h->ev1, h->stream));
             h->timedScan = h->timing;
         } else {
-            // groups of about a quarter of the call (2 .. VT_UP_GROUP batches): the first
-            // group's upload is the only one not hidden behind a scan, and a scan launch of
-            // >= 2 batches keeps the fused launch's efficiency
-            const int gb = std::min(nb, std::max(2, std::min(VT_UP_GROUP, nb / 4)));
+            // a first group of one batch (its upload is the only one not hidden behind a
+            // scan), then groups of about a third of the rest (2 .. VT_UP_GROUP batches: a
+            // scan launch of >= 2 batches keeps the fused launch's efficiency).  10 batches
+            // of 1,024 queries from a pageable array: groups (1, 3, 3, 3) 1.674 ms per call
+            // against 1.745 for (2, 2, 2, 2, 2), 1.759 for threes, 1.762 for fives, 1.920 for
+            // ones, and 1.757 with the caller's array page-locked for the call
+            // (hipHostRegister): the uploads are not the bound (tools/stream_ab.py --host)
+            const int gb = std::min(nb, std::max(2, std::min(VT_UP_GROUP, (nb - 1) / 3)));
             if (!h->ustream) {
                 RS_HIP(hipStreamCreateWithFlags(&h->ustream, hipStreamNonBlocking));
                 for (int i = 0; i < 2; ++i) {
@@ -1664,9 +1668,10 @@ int vt_match_stream_impl(rs_vt* h, int nb, int nq, const uint8_t* queries, uint6
                 for (int i = 0; i < 2; ++i) RS_HIP(hipMalloc(&h->dUp[i], qb * gb));
                 h->upCap = qb * gb;
             }
-            const int ng = (nb + gb - 1) / gb;
-            for (int g = 0; g < ng; ++g) {
-                const int b0 = g * gb, n = std::min(gb, nb - b0), bi = g & 1;
+            const int g1n = nb >= 4 ? 1 : gb;
+            for (int g = 0, b0 = 0, n = 0; b0 < nb; ++g, b0 += n) {
+                n = std::min(g == 0 ? g1n : gb, nb - b0);
+                const int bi = g & 1;
                 // the buffer's group before last has had its planes built
                 if (g >= 2) RS_HIP(hipStreamWaitEvent(h->ustream, h->evUsed[bi], 0));
                 RS_HIP(hipMemcpyAsync(h->dUp[bi], queries + qb * b0, qb * n, hipMemcpyHostToDevice, h->ustream));
