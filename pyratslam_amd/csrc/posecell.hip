@@ -1283,9 +1283,14 @@ __device__ inline int co_wrap(int a, int n) {
 template <typename T, typename V>
 __device__ inline void co_put(T* __restrict__ base, size_t e, V v, bool wt, int nbytes) {
     if (wt) {
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, nbytes, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)(e * sizeof(T)), 0, 16);
+        if constexpr (sizeof(V) == 8) {
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), r, (int)(e * sizeof(T)), 0, 16);
+        } else {
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, (int)(e * sizeof(T)), 0, 16);
+        }
         return;
     }
     (void)wt;
@@ -2161,16 +2166,21 @@ inline unsigned hf_magic(int d) { return (unsigned)(0xFFFFFFFFull / (unsigned)d 
 // arrive in scalar registers with the wave and the image's loads issue without a
 // kernel-argument round trip (two dependent ones before: the block count, then the
 // union, 0.84 us from the block's start to the DMA issue at 64 x 64 x 36).
-template <bool EXC>
+template <bool EXC, int TH>
 __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     const float* __restrict__ U, int xy, int gxnb, int ulo, int uext, unsigned mgx, unsigned muh,
     const double* __restrict__ part_in, int npart_in, float* __restrict__ Uo, double* __restrict__ part_out,
     unsigned long long* __restrict__ slot_prev, unsigned long long* __restrict__ slot_zero,
     const float* __restrict__ filt, int nf, PcCtlHalo ctl, SepKernel<float> k,
     unsigned long long* __restrict__ rec) {
-    constexpr int TH = HF_TH, NV = TH / 4;   // 16-byte pieces per theta column
-    static_assert(TH % 4 == 0, "theta columns of whole 16-byte pieces");
-    constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
+    // TH: 36 (configs[1], the ROS node: the tuned phases below), or another even extent up
+    // to HF_TH (18: configs[0]'s grid, 10: simulate.py's), whose theta columns are not
+    // whole 16-byte pieces: the image then loads in 4-byte pieces, the theta pass runs a
+    // thread per union cell (cell_pass below) and the theta filter in 2-layer groups
+    static_assert(TH % 2 == 0 && TH >= FL + HALF && TH <= HF_TH, "an even theta extent, 10 .. HF_TH");
+    constexpr bool V4 = TH % 4 == 0;
+    constexpr int PW = V4 ? 4 : 1, NV = TH / PW;   // image pieces (PW floats each) per theta column
+    constexpr int WBUF = HF_UMAX * TH + 64 * PW;   // union image [cell][layer] (+ a wave-instruction of slack)
     constexpr int YBUF = 2 * TH * HF_YL;
     constexpr int BBUF = WBUF > YBUF ? WBUF : YBUF;
     constexpr int PP = TH + 64;   // path outputs per cell: rows TH dwords apart modulo the 64 banks
@@ -2200,8 +2210,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     // they land first and the total is formed while the image is in flight
     double pt[4];
     pc_partials_issue(part_in, npart_in, pt);
-    // 1. the union image, issued first: piece p = tid + HF_NT * r is 16-byte piece p % NV
-    //    of union cell p / NV (cells row-major, UH per row), landing at s_b + 4p
+    // 1. the union image, issued first: piece p = tid + HF_NT * r is piece p % NV (PW
+    //    floats) of union cell p / NV (cells row-major, UH per row), landing at s_b + PW p
     if (dma) {
         constexpr int DC = HF_NT / NV, DL = HF_NT % NV, NR = (HF_UMAX * NV + HF_NT - 1) / HF_NT;
         // A lane walks its pieces with full-rate 32-bit arithmetic only (no 64-bit,
@@ -2221,10 +2231,11 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 if (i0 + lane < npc) {
                     int gc = uy0 + vi;
                     gc -= gc >= Y ? Y : 0;
-                    const unsigned boff = __umul24((unsigned)(rb + gc), (unsigned)(4 * TH)) + 16u * (unsigned)l4;
-                    __builtin_amdgcn_global_load_lds(
-                        (__attribute__((address_space(1))) const void*)(reinterpret_cast<const char*>(U) + boff),
-                        (__attribute__((address_space(3))) void*)(s_b + 4 * i0), 16, 0, 0);
+                    const unsigned boff = __umul24((unsigned)(rb + gc), (unsigned)(4 * TH)) + 4u * PW * (unsigned)l4;
+                    const auto gsrc = (__attribute__((address_space(1))) const void*)(reinterpret_cast<const char*>(U) + boff);
+                    const auto ldst = (__attribute__((address_space(3))) void*)(s_b + PW * i0);
+                    if constexpr (V4) __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
+                    else __builtin_amdgcn_global_load_lds(gsrc, ldst, 4, 0, 0);
                 }
             }
             l4 += DL;
@@ -2282,7 +2293,70 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     unsigned long long bk = 0ull;
     const bool want_key = slot_prev != nullptr;
     PC_STAMP(11, 0);
-    if (dma && !cwrap) {
+    // a thread per union cell (theta extents other than HF_TH; at HF_TH a union spanning
+    // a whole period, or one larger than the LDS-DMA image)
+    auto cell_passes = [&]() __attribute__((always_inline)) {
+        // a union spanning a whole period (the windows wrap inside it), or one larger
+        // than the LDS-DMA image (columns from memory): thread c takes union cell c's
+        // column, scales it, forms all TH theta-pass outputs in registers and stores
+        // those of the windows holding the cell (a lane outside a window stores into its
+        // own dump slot, so the layers' chains interleave with no exec changes)
+        auto cell_pass = [&](int c, auto wrap_c) __attribute__((always_inline)) {
+            constexpr bool WRAP = decltype(wrap_c)::value;
+            const int ui = c / UH, vi = c - ui * UH;
+            int gr = ux0 + ui, gc = uy0 + vi;
+            gr -= gr >= X ? X : 0;
+            gc -= gc >= Y ? Y : 0;
+            float p[TH];
+            // the column as 16-byte vectors (TH % 4 == 0) or 8-byte pairs (TH even: a
+            // column starts 8-byte aligned)
+            using CV = typename std::conditional<V4, co_f4, hf_f2>::type;
+            constexpr int CW = V4 ? 4 : 2;
+            auto rd = [&](const float* base) __attribute__((always_inline)) {
+                const CV* src = reinterpret_cast<const CV*>(base);
+#pragma unroll
+                for (int v = 0; v < TH / CW; ++v) {
+                    const CV x = src[v];
+#pragma unroll
+                    for (int w = 0; w < CW; ++w) p[CW * v + w] = x[w];
+                }
+            };
+            if (dma) rd(s_b + c * TH);
+            else rd(U + ((size_t)gr * Y + gc) * TH);
+            nrm(p);
+            if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
+                const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
+#pragma unroll
+                for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
+            }
+#pragma unroll
+            for (int j = 0; j < TH; ++j) {
+                const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
+                hf_f2 eg = {0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < FL; ++t) eg += gei[t] * p[(j + t + TH - HALF) % TH];
+                if constexpr (WRAP) {
+                    int rx = ui - sxj, ry = vi - syj;
+                    rx += rx < 0 ? UW : 0;
+                    ry += ry < 0 ? UH : 0;
+                    if ((unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W)
+                        s_tw[j * HF_WJ + rx * HF_WP + ry] = eg;
+                } else {
+                    const bool in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
+                    s_tw[in ? j * HF_WJ + (ui - sxj) * HF_WP + (vi - syj) : TH * HF_WJ + tid] = eg;
+                }
+            }
+        };
+        if (cwrap) {
+#pragma unroll 1
+            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::true_type{});
+        } else {
+#pragma unroll 1
+            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{});
+        }
+    };
+    if constexpr (TH == HF_TH) {
+      if (dma && !cwrap) {
         // the common case, read straight from the union image [cell][layer]: wave w < 8
         // takes window rows 4(w&3) .. +3 (a lane per window cell) through the layers
         // [18(w>>2), +18).  Layer j's window cell (rx, ry) is union cell (rx + sx_j,
@@ -2395,67 +2469,11 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 }
             }
         }
+      } else {
+        cell_passes();
+      }
     } else {
-        // a union spanning a whole period (the windows wrap inside it), or one larger
-        // than the LDS-DMA image (columns from memory): thread c takes union cell c's
-        // column, scales it, forms all TH theta-pass outputs in registers and stores
-        // those of the windows holding the cell (a lane outside a window stores into its
-        // own dump slot, so the layers' chains interleave with no exec changes)
-        auto cell_pass = [&](int c, auto wrap_c) __attribute__((always_inline)) {
-            constexpr bool WRAP = decltype(wrap_c)::value;
-            const int ui = c / UH, vi = c - ui * UH;
-            int gr = ux0 + ui, gc = uy0 + vi;
-            gr -= gr >= X ? X : 0;
-            gc -= gc >= Y ? Y : 0;
-            float p[TH];
-            if (dma) {
-                const co_f4* src = reinterpret_cast<const co_f4*>(s_b + c * TH);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const co_f4 x = src[v];
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
-                }
-            } else {
-                const co_f4* src = reinterpret_cast<const co_f4*>(U + ((size_t)gr * Y + gc) * TH);
-#pragma unroll
-                for (int v = 0; v < NV; ++v) {
-                    const co_f4 x = src[v];
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) p[4 * v + w] = x[w];
-                }
-            }
-            nrm(p);
-            if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
-                const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
-#pragma unroll
-                for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
-            }
-#pragma unroll
-            for (int j = 0; j < TH; ++j) {
-                const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
-                hf_f2 eg = {0.f, 0.f};
-#pragma unroll
-                for (int t = 0; t < FL; ++t) eg += gei[t] * p[(j + t + TH - HALF) % TH];
-                if constexpr (WRAP) {
-                    int rx = ui - sxj, ry = vi - syj;
-                    rx += rx < 0 ? UW : 0;
-                    ry += ry < 0 ? UH : 0;
-                    if ((unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W)
-                        s_tw[j * HF_WJ + rx * HF_WP + ry] = eg;
-                } else {
-                    const bool in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
-                    s_tw[in ? j * HF_WJ + (ui - sxj) * HF_WP + (vi - syj) : TH * HF_WJ + tid] = eg;
-                }
-            }
-        };
-        if (cwrap) {
-#pragma unroll 1
-            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::true_type{});
-        } else {
-#pragma unroll 1
-            for (int c = tid; c < nu; c += HF_NT) cell_pass(c, std::false_type{});
-        }
+        cell_passes();
     }
     PC_STAMP(11, 1);
     PC_STAMPW(12);
@@ -2467,12 +2485,14 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         cv -= cv >= Y ? Y : 0;
         if (cu >= UW || cv >= UH) {
             const unsigned lin0 = ((unsigned)(x0 + i) * Y + (y0 + j)) * TH;
-            const co_f4* src = reinterpret_cast<const co_f4*>(U + lin0);
+            using CV = typename std::conditional<V4, co_f4, hf_f2>::type;
+            constexpr int CW = V4 ? 4 : 2;
+            const CV* src = reinterpret_cast<const CV*>(U + lin0);
 #pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                const co_f4 x = src[v];
+            for (int v = 0; v < TH / CW; ++v) {
+                const CV x = src[v];
 #pragma unroll
-                for (int w = 0; w < 4; ++w) bk = max(bk, argmax_key(nrm(x[w]), lin0 + 4 * v + w));
+                for (int w = 0; w < CW; ++w) bk = max(bk, argmax_key(nrm(x[w]), lin0 + CW * v + w));
             }
         }
     }
@@ -2509,8 +2529,11 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             di[qc * HF_YC] = eg.y;
         }
     };
-    static_assert(TH == 36 && HF_W == 16 && HF_Q == 10 && HF_NW == 9, "phase 3's task split");
-    {
+    static_assert(HF_W == 16 && HF_Q == 10 && HF_NW == 9, "phase 3's task split");
+    if constexpr (TH != 36) {
+        for (int t = tid; t < TH * HF_W; t += HF_NT)
+            ytask(t >> 4, t & 15, std::integral_constant<int, 0>{}, std::integral_constant<int, HF_Q>{});
+    } else {
         using I = std::integral_constant<int, 0>;
         if (wave < 8) ytask(tid >> 4, tid & 15, I{}, std::integral_constant<int, HF_Q>{});
         const int jr = 32 + (lane >> 4), rr = lane & 15;
@@ -2560,9 +2583,14 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             }
         }
     };
-    static_assert(TH * HF_Q <= 6 * 64 && TH * HF_Q > 5 * 64, "phase 4's task split: 6 wave-tasks per half");
-    if (wave < 6) xtask(wave * 64 + lane, std::integral_constant<int, 0>{});
-    {
+    if constexpr (TH != 36) {
+        for (int t = tid; t < 2 * TH * HF_Q; t += HF_NT) {
+            if (t < TH * HF_Q) xtask(t, std::integral_constant<int, 0>{});
+            else xtask(t - TH * HF_Q, std::integral_constant<int, 1>{});
+        }
+    } else {
+        static_assert(TH * HF_Q <= 6 * 64 && TH * HF_Q > 5 * 64, "phase 4's task split: 6 wave-tasks per half");
+        if (wave < 6) xtask(wave * 64 + lane, std::integral_constant<int, 0>{});
         const int s1 = wave == 8 ? 0 : wave == 6 ? 1 : wave == 7 ? 2 : wave == 1 ? 3 : wave == 2 ? 4 : wave == 3 ? 5 : -1;
         if (s1 >= 0) xtask(s1 * 64 + lane, std::integral_constant<int, 1>{});
     }
@@ -2572,7 +2600,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     // within a relative 2^-20 of it (HF_NEAR): P = U * (1/t) rounds monotonically, so the
     // first maximum of P is the first maximum of U unless another cell lies that close
     unsigned long long rk = 0ull;
-    co_f4 uv = {0.f, 0.f, 0.f, 0.f};
+    co_f4 uv = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};   // (lanes past a 2-layer group's stay -inf)
     bool has_uv = false;
     // every thread's partial sum and key, past Q in s_t (free from here on): the last
     // wave, which has no task in phase 5, reduces them there -- lane l adds the values of
@@ -2640,42 +2668,52 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 if (j < FL) sp[HALF + TH + j] = v;
             }
         };
-        static_assert(TH == 36 && HF_T == 4, "phase 5's task split");
-        if (wave < 4) ptask(tid >> 3, tid & 3, 2 * ((tid >> 2) & 1), std::integral_constant<int, 2>{});
-        else if (wave == 5) ptask(32 + (lane >> 4), lane & 3, (lane >> 2) & 3, std::integral_constant<int, 1>{});
+        static_assert(HF_T == 4, "phase 5's task split");
+        if constexpr (TH != 36) {
+            for (int t = tid; t < TH * 8; t += HF_NT)
+                ptask(t >> 3, t & 3, 2 * ((t >> 2) & 1), std::integral_constant<int, 2>{});
+        } else {
+            if (wave < 4) ptask(tid >> 3, tid & 3, 2 * ((tid >> 2) & 1), std::integral_constant<int, 2>{});
+            else if (wave == 5) ptask(32 + (lane >> 4), lane & 3, (lane >> 2) & 3, std::integral_constant<int, 1>{});
+        }
         co_lds_barrier();
         PC_STAMP(7, 5);
-        // 6. theta filter (:310) + clamp (:314): task (cell, group of 4 layers) -> one
-        //    16-byte write-through store of U (normalised by the next launch)
+        // 6. theta filter (:310) + clamp (:314): task (cell, group of G layers) -> one
+        //    write-through store of U (normalised by the next launch): G = 4 (16 bytes),
+        //    or 2 (8 bytes) when TH is not a multiple of 4
         const int nbytes = (int)min((size_t)X * Y * TH * sizeof(float), (size_t)INT_MAX);
         const bool wt = (size_t)X * Y * TH * sizeof(float) <= (size_t)INT_MAX;
-        static_assert(HF_T * HF_T * NV <= HF_NT, "one theta-filter task per thread");
-        if (tid < HF_T * HF_T * NV) {
+        constexpr int G = V4 ? 4 : 2, NGR = TH / G, NRD = (G + 2 * HALF + G - 1) / G;
+        using GV = typename std::conditional<V4, co_f4, hf_f2>::type;
+        static_assert(HF_T * HF_T * NGR <= HF_NT, "one theta-filter task per thread");
+        if (tid < HF_T * HF_T * NGR) {
             const int t = tid;
-            const int cell = t / NV, g = t - cell * NV, ta = cell >> 2, tb = cell & 3;
+            const int cell = t / NGR, g = t - cell * NGR, ta = cell >> 2, tb = cell & 3;
             if (ta < tw && tb < tht) {
-            const co_f4* sv = reinterpret_cast<const co_f4*>(s_po + cell * PP + 4 * g);
-            float r[12];
+            const GV* sv = reinterpret_cast<const GV*>(s_po + cell * PP + G * g);
+            float r[NRD * G];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const co_f4 x = sv[q];
+            for (int q = 0; q < NRD; ++q) {
+                const GV x = sv[q];
 #pragma unroll
-                for (int w = 0; w < 4; ++w) r[4 * q + w] = x[w];
+                for (int w = 0; w < G; ++w) r[G * q + w] = x[w];
             }
-            co_f4 v;
+            GV v;
 #pragma unroll
-            for (int o = 0; o < 4; ++o) {
+            for (int o = 0; o < G; ++o) {
                 float x = 0.f;
 #pragma unroll
                 for (int z = 0; z < FL; ++z) x += r[o + z] * zf[z];
                 v[o] = pc_clamp(x);
             }
-            const unsigned lin = ((unsigned)(x0 + ta) * Y + (y0 + tb)) * TH + 4 * g;
+            const unsigned lin = ((unsigned)(x0 + ta) * Y + (y0 + tb)) * TH + G * g;
             co_put(Uo, lin, v, wt, nbytes);
             if (rec) {
 #pragma unroll
-                for (int o = 0; o < 4; ++o) rk = max(rk, argmax_key(v[o], lin + o));
-                uv = v;
+                for (int o = 0; o < G; ++o) {
+                    rk = max(rk, argmax_key(v[o], lin + o));
+                    uv[o] = v[o];
+                }
                 has_uv = true;
             }
             }
@@ -2727,6 +2765,18 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     }
     PC_STAMP(7, 6);
+}
+
+// The instances of pc_step_halo: HF_TH (configs[1], the ROS node) and the even extents
+// of configs[0]'s grid (18) and simulate.py's (10); pc_halo_fit admits these.
+inline bool hf_th_ok(int TH) { return TH == HF_TH || TH == 18 || TH == 10; }
+template <bool EXC, typename... A>
+void hf_launch(int TH, dim3 grid, hipStream_t st, A... a) {
+    switch (TH) {
+    case 18: hipLaunchKernelGGL((pc_step_halo<EXC, 18>), grid, dim3(HF_NT), 0, st, a...); break;
+    case 10: hipLaunchKernelGGL((pc_step_halo<EXC, 10>), grid, dim3(HF_NT), 0, st, a...); break;
+    default: hipLaunchKernelGGL((pc_step_halo<EXC, HF_TH>), grid, dim3(HF_NT), 0, st, a...); break;
+    }
 }
 
 // The end of a halo-form call: the normalised state P = U * (1/t) of the last step
@@ -3445,7 +3495,7 @@ int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
                                       : h->dPart + (size_t)(pend ? h->haloPart : 0) * h->nPart;
         const int npart_in = s > 0 || pend ? h->nPart : 0;
         if (pk) RS_HIP(hipEventRecord(h->evPool[2 * s], h->stream));
-        hipLaunchKernelGGL((pc_step_halo<false>), grid, dim3(HF_NT), 0, h->stream, buf[(c0 + s) & 1],
+        hf_launch<false>(h->TH, grid, h->stream, static_cast<const float*>(buf[(c0 + s) & 1]),
                            hf_pack(h->X, h->Y), hf_pack(h->cgx, grid.x), hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh),
                            hf_magic(h->cgx), hf_magic(c.uh), part_in, npart_in, buf[(c0 + s + 1) & 1],
                            h->dPart + (size_t)((p0 + s) & 1) * h->nPart,
@@ -3979,9 +4029,9 @@ bool pc_halo_fit(const rs_pc* h) {
     // (the union's origin and extent travel as 16-bit fields: make_ctl_halo, hf_pack)
     // (so do the grid, the tile count and the block count of pc_step_halo; tile / gx is a
     // high multiply valid below 2^16, hf_magic)
-    return h->esz == 4 && h->TH == HF_TH && h->X >= HF_W && h->Y >= HF_W && h->X <= 32767 && h->Y <= 32767 &&
+    return h->esz == 4 && hf_th_ok(h->TH) && h->X >= HF_W && h->Y >= HF_W && h->X <= 32767 && h->Y <= 32767 &&
            (size_t)((h->X + HF_T - 1) / HF_T) * ((h->Y + HF_T - 1) / HF_T) <= 65535 &&
-           h->nf <= RT_NFMAX && h->n * sizeof(float) <= (size_t)INT_MAX;
+           h->nf <= RT_NFMAX && h->n * sizeof(float) <= (size_t)INT_MAX && h->n % 4 == 0;   // (pc_halo_finish: float4s)
 }
 
 int pc_halo_set(rs_pc* h) {
@@ -4008,7 +4058,7 @@ int pc_choose_form(rs_pc* h) {
     if ((env == nullptr || env[0] == 0) && pc_halo_default(h)) return pc_halo_set(h);
     if (env && std::strcmp(env, "halo") == 0) {
         RS_CHECK(pc_halo_fit(h), RS_ERR_ARG,
-                 "RS_PC_FORM=halo needs float32, TH == %d, %d <= X, Y <= 32767 and at most %d path filters", HF_TH,
+                 "RS_PC_FORM=halo needs float32, TH 10, 18 or %d, %d <= X, Y <= 32767 and at most %d path filters", HF_TH,
                  HF_W, RT_NFMAX);
         return pc_halo_set(h);
     }
@@ -4274,7 +4324,7 @@ int rs_pc_excite(rs_pc* h) {
         PcCtlHalo c{};
         c.uw = (short)HF_W;
         c.uh = (short)HF_W;
-        hipLaunchKernelGGL((pc_step_halo<true>), dim3(h->cgx * h->cgy), dim3(HF_NT), 0, h->stream,
+        hf_launch<true>(h->TH, dim3(h->cgx * h->cgy), h->stream,
                            static_cast<const float*>(h->dP), hf_pack(h->X, h->Y), hf_pack(h->cgx, h->cgx * h->cgy),
                            hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), hf_magic(h->cgx), hf_magic(c.uh), h->dPart, 0,
                            static_cast<float*>(h->dQ), h->dPart, nullptr, nullptr, static_cast<const float*>(h->dFilt), h->nf, c, h->kf,

@@ -46,8 +46,10 @@ def own_argmax(net):
     return tuple(int(v) for v in np.unravel_index(np.argmax(p), p.shape)), p
 
 
-@pytest.mark.parametrize('name', ['pc64_s0', 'pc_ros21'])
+@pytest.mark.parametrize('name', ['pc64_s0', 'pc_ros21', 'pc32_s0', 'pc32_s1', 'pc32_s2', 'pc_simulate'])
 def test_golden_trajectory_per_step_and_batched(halo, name):
+    # (pc32_*: configs[0]'s 32 x 32 x 18; pc_simulate: simulate.py's 50 x 50 x 10 -- the
+    # instances whose theta columns are not whole 16-byte pieces)
     case = load_golden(name)
     shape = tuple(int(s) for s in case['shape'])
     net = halo(shape)
@@ -66,11 +68,12 @@ def test_golden_trajectory_per_step_and_batched(halo, name):
     assert np.abs(b.posecells - dense_state(case, n - 1)).max() < F32_TOL
 
 
-def test_network_death_vs_reference(halo):
-    """pc_death64 (made by the reference): the dead steps take the total == 0
+@pytest.mark.parametrize('name', ['pc_death64', 'pc_death32'])
+def test_network_death_vs_reference(halo, name):
+    """pc_death64 / pc_death32 (made by the reference): the dead steps take the total == 0
     branch and stay exactly zero, the peak of the all-zero volume is (0, 0, 0), a
     second inject revives it; per step and batched around the inject."""
-    case = load_golden('pc_death64')
+    case = load_golden(name)
     shape = tuple(int(s) for s in case['shape'])
     kill, revive = int(case['kill_step']), int(case['revive_step'])
     odom = case['odom']
@@ -95,7 +98,8 @@ def test_network_death_vs_reference(halo):
     assert np.abs(b.posecells - dense_state(case, len(odom) - 1)).max() < F32_TOL
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (17, 30, 36), (16, 16, 36), (128, 72, 36)])
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (17, 30, 36), (16, 16, 36), (128, 72, 36),
+                                   (32, 32, 18), (50, 50, 10), (18, 30, 18), (17, 28, 10)])
 def test_random_and_fast_odometry_vs_oracle(halo, shape):
     """Bench odometry mixed with fast steps (vtrans up to 2 m: shifts up to 10 cells,
     unions beyond the LDS-DMA image, which take the direct-load path), ragged tiles
@@ -316,7 +320,7 @@ def ambig_calls(net):
     return v.value
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36)])
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (32, 32, 18), (50, 50, 10)])
 def test_unnormalised_call_end_equals_settled(halo, shape):
     """A call leaves the state unnormalised and returns the last step's peak from the
     per-block records of U (pc_halo_export); the next call scales it on load.  Against a
@@ -347,7 +351,7 @@ def test_unnormalised_call_end_equals_settled(halo, shape):
     assert ambig_calls(a) == 0 and ambig_calls(b) == 0
 
 
-@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36)])
+@pytest.mark.parametrize('shape', [(64, 64, 36), (21, 21, 36), (32, 32, 18), (50, 50, 10)])
 def test_read_of_pending_state_settles_in_one_pass(halo, shape):
     """The ROS node's step: update() then a read of the volume.  The read of a state a
     call left unnormalised normalises it and writes the float64 volume in one pass

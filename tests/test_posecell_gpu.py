@@ -381,7 +381,10 @@ def test_default_form_by_grid_size(pcn, monkeypatch):
     assert pcn((21, 21, 36)).step_form() == 'halo'
     assert pcn((64, 64, 36), precision='float64').step_form() == 'rows'
     assert pcn((68, 64, 36)).step_form() == 'rows'       # 17 x 16 tiles: more than one per CU
-    assert pcn((32, 32, 18)).step_form() == 'rows'       # TH != 36
+    assert pcn((32, 32, 18)).step_form() == 'halo'       # configs[0]'s grid: TH = 18
+    assert pcn((50, 50, 10)).step_form() == 'halo'       # simulate.py's grid: TH = 10
+    assert pcn((21, 21, 18)).step_form() != 'halo'       # X * Y * TH not a multiple of 4
+    assert pcn((32, 32, 20)).step_form() != 'halo'       # no halo instance for TH = 20
     assert pcn((128, 128, 72)).step_form() == 'cols'
     assert pcn((128, 130, 72)).step_form() == 'stream'    # Y not a multiple of 4: no cols
     assert pcn((128, 128, 100)).step_form() == 'cols'     # theta extent beyond one block: chunked
