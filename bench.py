@@ -474,6 +474,31 @@ def bench_posecells(args, d):
     }
 
 
+def bench_other_grids(args, d):
+    """Batched run() at the reference's other grids: configs[0]'s 32x32x18 and
+    simulate.py's 50x50x10 (simulate.py:9), both one launch per step (the halo form's
+    18- and 10-layer instances since round 6; two launches per step before)."""
+    from pyratslam_amd import PoseCellNetwork, synthetic
+    out = {}
+    n = max(200, args.pc_steps // 5)
+    for shape in ((32, 32, 18), (50, 50, 10)):
+        net = PoseCellNetwork(shape, device=d.dev)
+        net.inject(1, tuple(s // 2 for s in shape))
+        od = synthetic.odometry(n + 200, seed=0)
+        net.run(od[:200])
+        d.barrier()
+        t0 = time.perf_counter()
+        net.run(od[200:200 + n])
+        t1 = time.perf_counter()
+        d.barrier()
+        dt = d.max(t1 - t0)
+        out['x'.join(map(str, shape))] = {'steps_per_s': n / dt, 'us_per_step': 1e6 * dt / n,
+                                          'steps': n, 'step_form': net.step_form(),
+                                          'finite': bool(np.isfinite(net.posecells).all())}
+        net.close()
+    return out
+
+
 def bench_node_step(args, d):
     """The ROS node's per-step drop-in cost (ros_simulate.py:134-145): update()
     and then a read of the whole ``.posecells`` volume (the node publishes it as a
@@ -693,6 +718,7 @@ def main():
                                  warmup=1, bps=2)
     pc = bench_posecells(args, d)
     pc['node_step'] = bench_node_step(args, d)
+    pc['other_grids'] = bench_other_grids(args, d)
     pcs, st = None, None
     if not args.no_pc_stress:
         pcs = bench_posecell_stress(args, d)
