@@ -185,7 +185,7 @@ int rs_pc_set_profiling(rs_pc* h, int enable);
 int rs_pc_kernel_ms(rs_pc* h, double ms[2]);
 /* step kernels in use: "rows" (row-tiled excite + path launches, Y <= 128),
  * "cols" (column tiles through all layers, large grids), "halo" (one launch per
- * step, the excitation recomputed on each tile's halo; float32, TH = 36), "stream"
+ * step, the excitation recomputed on each tile's halo; float32, TH = 36, 18 or 10), "stream"
  * (layer streaming, large grids outside the column form's limits) or "tiles" (3-D tiles) */
 const char* rs_pc_step_form(const rs_pc* h);
 /* Test hooks (no reference counterpart):
