@@ -2180,7 +2180,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     static_assert(TH % 2 == 0 && TH >= FL + HALF && TH <= HF_TH, "an even theta extent, 10 .. HF_TH");
     constexpr bool V4 = TH % 4 == 0;
     constexpr int PW = V4 ? 4 : 1, NV = TH / PW;   // image pieces (PW floats each) per theta column
-    constexpr int WBUF = HF_UMAX * TH + 64 * PW;   // union image [cell][layer] (+ a wave-instruction of slack)
+    constexpr int WBUF = HF_UMAX * TH + 64 * 4;   // union image [cell][layer] (+ a wave-instruction of slack)
     constexpr int YBUF = 2 * TH * HF_YL;
     constexpr int BBUF = WBUF > YBUF ? WBUF : YBUF;
     constexpr int PP = TH + 64;   // path outputs per cell: rows TH dwords apart modulo the 64 banks
@@ -2210,18 +2210,25 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     // they land first and the total is formed while the image is in flight
     double pt[4];
     pc_partials_issue(part_in, npart_in, pt);
-    // 1. the union image, issued first: piece p = tid + HF_NT * r is piece p % NV (PW
-    //    floats) of union cell p / NV (cells row-major, UH per row), landing at s_b + PW p
-    if (dma) {
-        constexpr int DC = HF_NT / NV, DL = HF_NT % NV, NR = (HF_UMAX * NV + HF_NT - 1) / HF_NT;
+    // 1. the union image, issued first: piece p = tid + HF_NT * r is piece p % NVU of union
+    //    unit p / NVU (a unit: UC cells of one union row, units row-major, UH / UC per row),
+    //    landing at s_b + PWU p.  TH % 4 == 0: a unit is a cell of TH / 4 16-byte pieces.
+    //    Otherwise, when the host made the union's start column and width even (and Y is
+    //    even: make_ctl_halo), a unit is a cell pair, 2 TH floats from an even cell, 16-byte
+    //    aligned (TH / 2 16-byte pieces); else a cell of TH 4-byte pieces.
+    auto issue = [&](auto pw_c, auto nvu_c, auto uc_c) __attribute__((always_inline)) {
+        constexpr int PWU = decltype(pw_c)::value, NVU = decltype(nvu_c)::value, UC = decltype(uc_c)::value;
+        constexpr int DC = HF_NT / NVU, DL = HF_NT % NVU, NR = (HF_UMAX / UC * NVU + HF_NT - 1) / HF_NT;
         // A lane walks its pieces with full-rate 32-bit arithmetic only (no 64-bit,
         // quarter-rate address math; measured neutral: the issue, about 0.95 us from the
         // block's start at 64 x 64 x 36, is not VALU-bound, r4 probe): the row's first cell rb =
         // gr * Y carried incrementally (the union row advances by dU or dU + 1 < X per
         // round and UW <= X, so one wrap suffices), a 32-bit byte offset from the state's
-        // base (n * 4 <= INT_MAX, pc_halo_fit) by a 24-bit multiply (cells < 2^24)
-        const int npc = nu * NV, dU = (int)__umulhi((unsigned)DC, muh), dV = DC - dU * UH, XY = X * Y;
-        int c = tid / NV, l4 = tid - c * NV, ui = (int)__umulhi((unsigned)c, muh), vi = c - ui * UH;
+        // base (n * 4 <= INT_MAX, pc_halo_fit) by a 24-bit multiply (cells < 2^24).
+        // Units per row: UH / UC, by the same high multiply (UC c / UH, c < 2^15)
+        const int UHU = UH / UC, npc = nu / UC * NVU, XY = X * Y;
+        const int dU = (int)__umulhi((unsigned)(UC * DC), muh), dV = DC - dU * UHU;
+        int c = tid / NVU, l4 = tid - c * NVU, ui = (int)__umulhi((unsigned)(UC * c), muh), vi = c - ui * UHU;
         int rb = ux0 + ui;
         rb = (rb >= X ? rb - X : rb) * Y;
 #pragma unroll
@@ -2229,27 +2236,38 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             const int i0 = r * HF_NT + wave * 64;  // wave-uniform
             if (i0 < npc) {
                 if (i0 + lane < npc) {
-                    int gc = uy0 + vi;
+                    int gc = uy0 + UC * vi;
                     gc -= gc >= Y ? Y : 0;
-                    const unsigned boff = __umul24((unsigned)(rb + gc), (unsigned)(4 * TH)) + 4u * PW * (unsigned)l4;
+                    const unsigned boff = __umul24((unsigned)(rb + gc), (unsigned)(4 * TH)) + 4u * PWU * (unsigned)l4;
                     const auto gsrc = (__attribute__((address_space(1))) const void*)(reinterpret_cast<const char*>(U) + boff);
-                    const auto ldst = (__attribute__((address_space(3))) void*)(s_b + PW * i0);
-                    if constexpr (V4) __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
+                    const auto ldst = (__attribute__((address_space(3))) void*)(s_b + PWU * i0);
+                    if constexpr (PWU == 4) __builtin_amdgcn_global_load_lds(gsrc, ldst, 16, 0, 0);
                     else __builtin_amdgcn_global_load_lds(gsrc, ldst, 4, 0, 0);
                 }
             }
             l4 += DL;
             vi += dV;
             rb += dU * Y;
-            if (l4 >= NV) {
-                l4 -= NV;
+            if (l4 >= NVU) {
+                l4 -= NVU;
                 ++vi;
             }
-            if (vi >= UH) {
-                vi -= UH;
+            if (vi >= UHU) {
+                vi -= UHU;
                 rb += Y;
             }
             rb -= rb >= XY ? XY : 0;
+        }
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    if (dma) {
+        if constexpr (V4) {
+            issue(I4{}, std::integral_constant<int, TH / 4>{}, I1{});
+        } else {
+            if (((cuy | UH | Y) & 1) == 0) issue(I4{}, std::integral_constant<int, TH / 2>{}, I2{});
+            else issue(I1{}, std::integral_constant<int, TH>{}, I1{});
         }
     }
     PC_STAMP(10, 0);
@@ -3298,17 +3316,30 @@ void make_ctl_halo(const rs_pc* h, int s, const int32_t* ox, const int32_t* oy, 
         mny = std::min(mny, cy);
         mxy = std::max(mxy, cy);
     }
+    const int uw = std::min(HF_W + mxx - mnx, h->X);
+    int uy = mny, uh = std::min(HF_W + mxy - mny, h->Y);
+    const bool wrap = HF_W + mxx - mnx > h->X || HF_W + mxy - mny > h->Y;
+    // theta extents that are not whole 16-byte pieces (pc_step_halo loads the image in
+    // 16-byte pieces of cell pairs then): an even start column and width, one column more
+    // on either side where needed, when that stays a union the image holds
+    if (h->TH % 4 != 0 && h->Y % 2 == 0 && !wrap) {
+        const int py = uy - (uy & 1), ph = (uh + (uy & 1) + 1) & ~1;
+        if (ph <= h->Y && uw * ph <= HF_UMAX) {
+            uy = py;
+            uh = ph;
+        }
+    }
     for (int k = 0; k < h->TH; ++k) {
         c->sx[k] = (short)(co_centre(ox[b + k], h->X) - mnx);
-        c->sy[k] = (short)(co_centre(oy[b + k], h->Y) - mny);
+        c->sy[k] = (short)(co_centre(oy[b + k], h->Y) - uy);
         c->fo[k] = (unsigned char)fidx[b + k];
     }
     for (int z = 0; z < FL; ++z) c->zf[z] = (float)zf[(size_t)s * FL + z];
     c->ux = (short)mnx;
-    c->uy = (short)mny;
-    c->uw = (short)std::min(HF_W + mxx - mnx, h->X);
-    c->uh = (short)std::min(HF_W + mxy - mny, h->Y);
-    c->wrap = HF_W + mxx - mnx > h->X || HF_W + mxy - mny > h->Y;
+    c->uy = (short)uy;
+    c->uw = (short)uw;
+    c->uh = (short)uh;
+    c->wrap = wrap;
 }
 
 // Where step s of a launch sequence leaves its results: its RES_SLOTS argmax
