@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "rs_common.h"
@@ -3186,37 +3187,50 @@ namespace {
 // forms; the others keep P layer-major
 inline bool pc_thfast(const rs_pc* h) { return h->cols || h->halo; }
 
-int pc_grow_steps(rs_pc* h, int n) {
-    if (n <= h->ctlCap && n <= h->resCap) return RS_OK;
-    int cap = h->ctlCap > 0 ? h->ctlCap : 16;
-    while (cap < n) cap *= 2;
-    if (h->dCtl) RS_HIP(hipFree(h->dCtl));
-    if (h->hCtl) RS_HIP(hipHostFree(h->hCtl));
-    if (h->dRes) RS_HIP(hipFree(h->dRes));
-    if (h->hRes) RS_HIP(hipHostFree(h->hRes));
-    if (h->dArgV) RS_HIP(hipFree(h->dArgV));
-    if (h->dArgI) RS_HIP(hipFree(h->dArgI));
-    h->dCtl = nullptr; h->hCtl = nullptr; h->dRes = nullptr; h->hRes = nullptr; h->hResDev = nullptr;
-    h->dArgV = nullptr; h->dArgI = nullptr;
-    RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
-    RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
-    RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
-    // every slot starts zeroed (the excitation's block 0 zeroes a step's slots again
-    // before its path kernel max-reduces into them; no step ever reads freed data)
-    RS_HIP(hipMemsetAsync(h->dRes, 0, sizeof(unsigned long long) * RES_SLOTS * cap, h->stream));
-    // the export kernel stores each step's key here with a system-scope store:
-    // fine-grained (coherent) host memory, so the store is visible once the stream
-    // has synchronised; pc_run_impl also checks a sentinel per step (RES_NONE)
-    RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap,
-                         hipHostMallocMapped | hipHostMallocCoherent));
-    for (int s = 0; s < cap; ++s) h->hRes[s] = RES_NONE;
-    RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hResDev), h->hRes, 0));
-    if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
-        RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
-        RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
+// Per-step buffers of a call of n steps, grown in powers of two: the result slots and
+// words always; the control ring (pinned staging + device copy, ctlStride bytes a step)
+// only for the forms that read it (ctl): the halo and column forms take each step's
+// control as kernel arguments, and a 10,000-step batch's 16 MiB of pinned ring was a
+// few milliseconds of page-locking inside its first call.
+int pc_grow_steps(rs_pc* h, int n, bool ctl = true) {
+    if (n > h->resCap) {
+        int cap = h->resCap > 0 ? h->resCap : 16;
+        while (cap < n) cap *= 2;
+        if (h->dRes) RS_HIP(hipFree(h->dRes));
+        if (h->hRes) RS_HIP(hipHostFree(h->hRes));
+        if (h->dArgV) RS_HIP(hipFree(h->dArgV));
+        if (h->dArgI) RS_HIP(hipFree(h->dArgI));
+        h->dRes = nullptr; h->hRes = nullptr; h->hResDev = nullptr;
+        h->dArgV = nullptr; h->dArgI = nullptr;
+        h->resCap = 0;
+        RS_HIP(hipMalloc(&h->dRes, sizeof(unsigned long long) * RES_SLOTS * cap));
+        // every slot starts zeroed (the excitation's block 0 zeroes a step's slots again
+        // before its path kernel max-reduces into them; no step ever reads freed data)
+        RS_HIP(hipMemsetAsync(h->dRes, 0, sizeof(unsigned long long) * RES_SLOTS * cap, h->stream));
+        // the export kernel stores each step's key here with a system-scope store:
+        // fine-grained (coherent) host memory, so the store is visible once the stream
+        // has synchronised; pc_run_impl also checks a sentinel per step (RES_NONE)
+        RS_HIP(hipHostMalloc(&h->hRes, sizeof(unsigned long long) * cap,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        for (int s = 0; s < cap; ++s) h->hRes[s] = RES_NONE;
+        RS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hResDev), h->hRes, 0));
+        if (h->prec == RS_PREC_F64) {  // float64 argmax: per-block partials + pc_argmax_steps
+            RS_HIP(hipMalloc(&h->dArgV, h->esz * (size_t)cap * h->nPathBlocks));
+            RS_HIP(hipMalloc(&h->dArgI, sizeof(unsigned) * (size_t)cap * h->nPathBlocks));
+        }
+        h->resCap = cap;
     }
-    h->ctlCap = cap;
-    h->resCap = cap;
+    if (ctl && n > h->ctlCap) {
+        int cap = h->ctlCap > 0 ? h->ctlCap : 16;
+        while (cap < n) cap *= 2;
+        if (h->dCtl) RS_HIP(hipFree(h->dCtl));
+        if (h->hCtl) RS_HIP(hipHostFree(h->hCtl));
+        h->dCtl = nullptr; h->hCtl = nullptr;
+        h->ctlCap = 0;
+        RS_HIP(hipMalloc(&h->dCtl, h->ctlStride * cap));
+        RS_HIP(hipHostMalloc(&h->hCtl, h->ctlStride * cap, hipHostMallocDefault));
+        h->ctlCap = cap;
+    }
     return RS_OK;
 }
 
@@ -3501,7 +3515,7 @@ int pc_halo_settle_read(rs_pc* h, double* xp_dev, bool* done) {
 // exports.  One host sync (two for RES_AMBIG).  RS_PC_HALO_SETTLE=1 always finishes.
 int pc_run_halo(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32_t* fidx,
                 const double* zf, int32_t* out_xyz) {
-    RS_TRY(pc_grow_steps(h, n));
+    RS_TRY(pc_grow_steps(h, n, false));   // (the control travels as kernel arguments)
     const bool pk = h->profiling && h->profKernels;
     if (pk) RS_TRY(pc_ensure_events(h, (size_t)2 * n + 2));
     for (int s = 0; s < n; ++s) h->hRes[s] = RES_NONE;
@@ -3803,12 +3817,12 @@ int pc_run_direct(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const i
                   const double* zf, int32_t* out_xyz) {
     if (n == 0) return RS_OK;
     if (h->halo) return pc_run_halo(h, n, ox, oy, fidx, zf, out_xyz);
-    RS_TRY(pc_grow_steps(h, n));
     // Batches: the column form takes each step's control as kernel arguments too (its
     // path kernel then starts its window loads without a global round trip for the
     // shifts: 128x128x72 27.5 -> 27.1 us per step with the filter table staged behind
     // the window); the other forms read the device ring
     const bool inline_ctl = (n == 1 || h->cols) && h->TH <= CTL_INLINE_MAX;
+    RS_TRY(pc_grow_steps(h, n, !inline_ctl));
     if (!inline_ctl) {
         RS_TRY(pc_pack_ctl(h, n, ox, oy, fidx, zf));
         RS_HIP(hipMemcpyAsync(h->dCtl, h->hCtl, h->ctlStride * n, hipMemcpyHostToDevice,
@@ -3919,8 +3933,8 @@ int pc_run_impl(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int
 // the theta origin or a shift lies outside what the tables cover.
 constexpr double PC_LUT_PRECISION = 10.0;  // filter_dict_2d_precision, posecell_network.py:48
 
-int pc_odom_control(const OdoTables* h, double vtrans, double vrot, int32_t* ox, int32_t* oy,
-                    int32_t* rows, double* zf) {
+static inline __attribute__((always_inline)) int pc_odom_control_body(const OdoTables* h, double vtrans, double vrot,
+                                                                      int32_t* ox, int32_t* oy, int32_t* rows, double* zf) {
 #pragma clang fp contract(off)
     const double vt = vtrans / h->vtScale;
     const double vr = vrot / h->vrScale;
@@ -3948,6 +3962,23 @@ int pc_odom_control(const OdoTables* h, double vtrans, double vrot, int32_t* ox,
     const double* f = h->zfTab + (size_t)((int)zo - h->zMin) * FL;
     for (int t = 0; t < FL; ++t) zf[t] = f[t];
     return RS_OK;
+}
+// The same operations compiled for SSE4.1 (nearbyint, trunc and floor become roundsd
+// with the same IEEE results: 0.80 -> 0.42 us per 72-layer step on the build host), used
+// when the CPU has it
+__attribute__((target("sse4.1"))) int pc_odom_control_sse41(const OdoTables* h, double vtrans, double vrot,
+                                                           int32_t* ox, int32_t* oy, int32_t* rows, double* zf) {
+    return pc_odom_control_body(h, vtrans, vrot, ox, oy, rows, zf);
+}
+int pc_odom_control_base(const OdoTables* h, double vtrans, double vrot, int32_t* ox, int32_t* oy, int32_t* rows,
+                         double* zf) {
+    return pc_odom_control_body(h, vtrans, vrot, ox, oy, rows, zf);
+}
+int pc_odom_control(const OdoTables* h, double vtrans, double vrot, int32_t* ox, int32_t* oy, int32_t* rows,
+                    double* zf) {
+    static const bool sse41 = __builtin_cpu_supports("sse4.1");
+    return sse41 ? pc_odom_control_sse41(h, vtrans, vrot, ox, oy, rows, zf)
+                 : pc_odom_control_base(h, vtrans, vrot, ox, oy, rows, zf);
 }
 
 template <typename T>
@@ -4479,16 +4510,45 @@ int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* f
     h->cOy.resize(th * (n > 0 ? n : 1));
     h->cRows.resize(th * (n > 0 ? n : 1));
     h->cZf.resize((size_t)FL * (n > 0 ? n : 1));
-    int todo = n;
-    for (int s = 0; s < n; ++s) {
-        const int st = pc_odom_control(&h->odo, odom[2 * s], odom[2 * s + 1], h->cOx.data() + th * s,
-                                       h->cOy.data() + th * s, h->cRows.data() + th * s,
-                                       h->cZf.data() + (size_t)FL * s);
-        if (st == RS_ERR_LUT_KEY) {
-            todo = s;
-            break;
+    // The batch's control is formed before its first launch (the step kernels take it as
+    // kernel arguments), so a long batch forms it on a few threads, each a contiguous range
+    // of steps: 10,000 steps at 128x128x72 spent about 6 ms on one (0.6 us per step of the
+    // 15 us step, added to the batch's wall time).  The first failing step decides, as in
+    // order on one thread.
+    int fail = n, fail_st = RS_OK;
+    auto range = [&](int s0, int s1, int* fs, int* fst) {
+        for (int s = s0; s < s1; ++s) {
+            const int st = pc_odom_control(&h->odo, odom[2 * s], odom[2 * s + 1], h->cOx.data() + th * s,
+                                           h->cOy.data() + th * s, h->cRows.data() + th * s,
+                                           h->cZf.data() + (size_t)FL * s);
+            if (st != RS_OK) {
+                *fs = s;
+                *fst = st;
+                return;
+            }
         }
-        RS_CHECK(st == RS_OK, st, "odometry of step %d outside the control tables", s);
+    };
+    const int nthr = n >= 1024 ? std::min(8, n / 512) : 1;
+    if (nthr > 1) {
+        std::vector<int> fs(nthr, n), fst(nthr, RS_OK);
+        std::vector<std::thread> pool;
+        const int per = (n + nthr - 1) / nthr;
+        for (int t = 1; t < nthr; ++t)
+            pool.emplace_back(range, std::min(n, t * per), std::min(n, (t + 1) * per), &fs[t], &fst[t]);
+        range(0, std::min(n, per), &fs[0], &fst[0]);
+        for (auto& th_ : pool) th_.join();
+        for (int t = 0; t < nthr; ++t)
+            if (fs[t] < fail) {
+                fail = fs[t];
+                fail_st = fst[t];
+            }
+    } else {
+        range(0, n, &fail, &fail_st);
+    }
+    int todo = n;
+    if (fail < n) {
+        if (fail_st == RS_ERR_LUT_KEY) todo = fail;
+        else RS_CHECK(false, fail_st, "odometry of step %d outside the control tables", fail);
     }
     RS_TRY(pc_run_impl(h, todo, h->cOx.data(), h->cOy.data(), h->cRows.data(), h->cZf.data(),
                        out_xyz));
