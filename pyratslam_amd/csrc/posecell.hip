@@ -4533,8 +4533,13 @@ int rs_pc_run_odom(rs_pc* h, int n, const double* odom, int32_t* out_xyz, int* f
         std::vector<int> fs(nthr, n), fst(nthr, RS_OK);
         std::vector<std::thread> pool;
         const int per = (n + nthr - 1) / nthr;
-        for (int t = 1; t < nthr; ++t)
-            pool.emplace_back(range, std::min(n, t * per), std::min(n, (t + 1) * per), &fs[t], &fst[t]);
+        for (int t = 1; t < nthr; ++t) {
+            try {
+                pool.emplace_back(range, std::min(n, t * per), std::min(n, (t + 1) * per), &fs[t], &fst[t]);
+            } catch (...) {   // no thread to be had: this one takes the range
+                range(std::min(n, t * per), std::min(n, (t + 1) * per), &fs[t], &fst[t]);
+            }
+        }
         range(0, std::min(n, per), &fs[0], &fst[0]);
         for (auto& th_ : pool) th_.join();
         for (int t = 0; t < nthr; ++t)
