@@ -243,7 +243,7 @@ int main(int argc, char** argv) {
         make_ctl_halo(h, 0, ox.data(), oy.data(), f.data(), zf.data(), &c);
         CK(hipEventRecord(c0, h->stream));
         for (int i = 0; i < reps; ++i)
-            hipLaunchKernelGGL((pc_step_halo<false, HF_TH>), g, b, 0, h->stream, (const float*)h->dP, hf_pack(X, Y),
+            hf_launch<false>(h->TH, g, h->stream, (const float*)h->dP, hf_pack(X, Y),
                                hf_pack(h->cgx, g.x), hf_pack(c.ux, c.uy), hf_pack(c.uw, c.uh), hf_magic(h->cgx),
                                hf_magic(c.uh), h->dPart, h->nPart, (float*)h->dQ, h->dPart + h->nPart, h->dRes, h->dRes + RES_SLOTS,
                                (const float*)h->dFilt, h->nf, c, h->kf, nullptr);
