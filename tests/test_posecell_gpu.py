@@ -270,6 +270,28 @@ def test_keyerror_leaves_reference_state(pcn, monkeypatch, form):
     assert np.abs(net2.posecells - ref2.posecells).max() < F64_TOL
 
 
+def test_keyerror_late_in_a_long_batch(pcn):
+    """A batch of 3,000 steps forms its control on several host threads (rs_pc_run_odom,
+    one contiguous range of steps each); the LUT KeyError of step 2,500 (pc_keyerror's
+    odometry) must stop the batch exactly as in order: steps 0 .. 2,499 run, then steps
+    1-4 of the bad one, then KeyError -- the same state as the steps taken one by one."""
+    case = load_golden('pc_keyerror')
+    shape = tuple(case['shape'])
+    od = odometry(3000, 5)
+    od[2500] = case['odom'][0]
+    a = pcn(shape, precision='float64')
+    b = pcn(shape, precision='float64')
+    for n in (a, b):
+        n.inject(1, (16, 16, 9))
+    with pytest.raises(KeyError):
+        a.run(od)
+    mb = b.run(od[:2500])
+    with pytest.raises(KeyError):
+        b.update(od[2500])
+    assert tuple(mb[-1]) == a.max_pc
+    assert np.array_equal(a.posecells, b.posecells)
+
+
 # the default form at 21x21x36, and the column form (P theta-fastest) at a ragged
 # grid whose theta extent is not a multiple of the 16-byte groups
 @pytest.mark.parametrize('form,shape', [('', (21, 21, 36)), ('cols', (24, 40, 13)), ('cols', (32, 32, 20))])
