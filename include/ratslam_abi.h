@@ -135,7 +135,9 @@ int rs_pc_run(rs_pc* h, int n, const int32_t* ox, const int32_t* oy, const int32
  * outside the uploaded filters (the caller then computes the control itself).
  * rs_pc_run_odom: odom[n*2] = (vtrans, vrot) per step; on a LUT miss at step s it
  * runs steps < s, then steps 1-4 of s, sets *first_bad = s and returns
- * RS_ERR_LUT_KEY (else *first_bad = -1). */
+ * RS_ERR_LUT_KEY (else *first_bad = -1).  A batch of 1,024 steps or more forms its
+ * control on up to 8 host threads before its first launch (the same values; the
+ * first failing step decides, as in order). */
 int rs_pc_set_odometry_tables(rs_pc* h, double vtrans_scale, double vrot_scale,
                               const double* cos_a, const double* sin_a, int key_min,
                               int nkeys, const int32_t* key_rows, int zorig_min, int nz,
