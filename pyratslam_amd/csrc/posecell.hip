@@ -1385,14 +1385,16 @@ __global__ __launch_bounds__(64 * NW) void pc_excite_cols(const T* __restrict__ 
     // outputs go to LDS as [r][c][L].
     if constexpr (FIX_TH > 0) {
         // the fixed-extent instance: 16-byte loads of 4 consecutive layers of a cell
-        // (a quarter of the load instructions), task (row r, half h of the row's
-        // outputs, layer group g): 10 window cells, 4 outputs x 4 layers, each output
-        // one 16-byte LDS store; 14 x 2 x TH/4 tasks (504 at TH = 72: 8 waves)
-        constexpr int NG = FIX_TH / 4, TH2 = TY / 2, HW = TH2 + 2 * HALF;
-        static_assert(HX * 2 * NG <= NT, "one task per thread");
+        // (a quarter of the load instructions), task (row r, layer group g): the row's
+        // 14 window cells, 8 outputs x 4 layers, each output one 16-byte LDS store;
+        // 14 x TH/4 tasks (252 at TH = 72: 4 waves).  (Half rows on 8 waves loaded 20
+        // cells a row, 80 KiB a block through the load path instead of 56: 14.53 ->
+        // 14.42 us per 128 x 128 x 72 step, tools/pc_ab.py, round 6)
+        constexpr int NG = FIX_TH / 4, TH2 = TY, HW = TH2 + 2 * HALF;
+        static_assert(HX * NG <= NT, "one task per thread");
         const int t = tid;
-        if (t < HX * 2 * NG) {
-            const int r = t / (2 * NG), rem = t - r * (2 * NG), h = rem / NG, g = rem - h * NG;
+        if (t < HX * NG) {
+            const int r = t / NG, h = 0, g = t - r * NG;
             const T* rowp = P + ((size_t)co_wrap(x0 - HALF + r, X) * Y) * FIX_TH + 4 * g;
             V w[HW];
 #pragma unroll
