@@ -181,25 +181,31 @@ def test_poisoned_scratch_first_updates_vs_c_oracle(halo):
         net.close()
 
 
-def test_keyerror_leaves_reference_state(halo):
+@pytest.mark.parametrize('shape', [(64, 64, 36), (32, 32, 18), (50, 50, 10)])
+def test_keyerror_leaves_reference_state(halo, shape):
     """vtrans 0.1 m = half a cell: the layer at heading 0 has residual +0.5, key 5,
-    the reference's KeyError((5, 5)) after steps 1-4 (posecell_network.py:249)."""
-    shape = (64, 64, 36)
+    the reference's KeyError((5, 5)) after steps 1-4 (posecell_network.py:249); the
+    excitation-only instance of each theta extent."""
     net = halo(shape)
-    net.inject(1, (32, 32, 18))
+    loc = tuple(x // 2 for x in shape)
+    net.inject(1, loc)
     with pytest.raises(KeyError) as e:
         net.update((0.1, 0.0))
-    assert e.value.args[0] == (5, 5)
     ref = P.PoseCellOracle(shape)
-    ref.inject(1, (32, 32, 18))
+    ref.inject(1, loc)
+    with pytest.raises(KeyError) as e_ref:
+        P.PoseCellOracle(shape).update((0.1, 0.0))
+    assert e.value.args[0] == e_ref.value.args[0]
+    if shape[2] == 36:
+        assert e.value.args[0] == (5, 5)
     ref.excite_inhibit_normalise()
     assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
     net2 = halo(shape)
-    net2.inject(1, (32, 32, 18))
+    net2.inject(1, loc)
     with pytest.raises(KeyError):
         net2.run([[0.2, 0.0], [0.3, 0.01], [0.1, 0.0]])
     ref2 = P.PoseCellOracle(shape)
-    ref2.inject(1, (32, 32, 18))
+    ref2.inject(1, loc)
     ref2.update((0.2, 0.0))
     ref2.update((0.3, 0.01))
     ref2.excite_inhibit_normalise()
