@@ -31,3 +31,13 @@ def dense_state(case, step):
 @pytest.fixture(scope='session')
 def golden():
     return load_golden
+
+
+def nonfinite_state(case, i):
+    """pc_nonfinite: the reference's state after the ValueError of vtrans case i."""
+    shape = tuple(int(s) for s in case['shape'])
+    off = int(case['vtrans_nnz'][:i].sum())
+    n = int(case['vtrans_nnz'][i])
+    out = np.zeros(int(np.prod(shape)))
+    out[case['vtrans_coo_idx'][off:off + n]] = case['vtrans_coo_val'][off:off + n]
+    return out.reshape(shape)

@@ -484,11 +484,79 @@ def gen_death(pn, out):
                             revive_step=np.int64(revive_at), revive=np.array(revive, dtype=np.int64))
 
 
+class _Py2Math(types.ModuleType):
+    """``math`` with Python 2's floor on non-finite arguments: Python 2's math.floor
+    returned a float, so a NaN or infinite argument came back as it was, where
+    Python 3's raises (posecell_network.py:304, the theta origin of a NaN or infinite
+    vrot).  Finite arguments floor as before."""
+    def __init__(self):
+        super().__init__('math')
+        for k in dir(math):
+            if not k.startswith('__') and k != 'floor':
+                setattr(self, k, getattr(math, k))
+
+    @staticmethod
+    def floor(x):
+        if isinstance(x, (float, np.floating)) and not math.isfinite(x):
+            return x
+        return math.floor(x)
+
+
+def gen_nonfinite(pn, out):
+    """Non-finite odometry, run by the reference: a NaN or
+    infinite vrot raises nothing and its all-NaN theta filter leaves a NaN volume for
+    good (peak: numpy's first NaN, (0, 0, 0)); a NaN or infinite vtrans raises
+    ValueError at the LUT lookup (int() of a NaN residual, :246-249) after steps 1-4,
+    whose state is stored.  With the Python 2 floor of the theta origin above."""
+    saved = builtins.math
+    builtins.math = _Py2Math()
+    try:
+        shape, loc = (32, 32, 18), (16, 16, 9)
+        arrays = {'shape': np.array(shape, dtype=np.int64), 'inject': np.array(loc, dtype=np.int64)}
+        vr_cases = [float('nan'), float('-inf')]
+        vr_max, vr_nan = [], []
+        for vr in vr_cases:
+            net = pn.PoseCellNetwork(shape)
+            net.inject(1, loc)
+            maxes, alln = [], []
+            for v in ((0.2, 0.01), (0.3, vr), (0.2, 0.0), (0.25, 0.1)):
+                net.update(v)
+                maxes.append(net.max_pc)
+                alln.append(bool(np.isnan(net.posecells).all()))
+            vr_max.append(maxes)
+            vr_nan.append(alln)
+        arrays.update(vrot=np.array(vr_cases), vrot_odom_other=np.array([[0.2, 0.01], [0.3, 0.0], [0.2, 0.0],
+                                                                           [0.25, 0.1]]),
+                      vrot_max_pc=np.array(vr_max, dtype=np.int64), vrot_all_nan=np.array(vr_nan))
+        vt_cases = [float('nan'), float('inf')]
+        raised, idxs, vals, nnz, pre = [], [], [], [], []
+        for vt in vt_cases:
+            net = pn.PoseCellNetwork(shape)
+            net.inject(1, loc)
+            net.update((0.2, 0.01))
+            pre.append(net.max_pc)
+            try:
+                net.update((vt, 0.0))
+                raised.append('')
+            except ValueError as e:
+                raised.append(type(e).__name__)
+            i, x = coo(net.posecells)
+            idxs.append(i)
+            vals.append(x)
+            nnz.append(len(i))
+        arrays.update(vtrans=np.array(vt_cases), vtrans_raised=np.array(raised),
+                      vtrans_pre_max_pc=np.array(pre, dtype=np.int64), vtrans_nnz=np.array(nnz, dtype=np.int64),
+                      vtrans_coo_idx=np.concatenate(idxs), vtrans_coo_val=np.concatenate(vals))
+        np.savez_compressed(os.path.join(out, 'pc_nonfinite.npz'), **arrays)
+    finally:
+        builtins.math = saved
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default=os.path.dirname(os.path.abspath(__file__)))
     ap.add_argument('--only', choices=['kernels', 'posecell', 'templates', 'float_pairs',
-                                       'ros_replay', 'death'])
+                                       'ros_replay', 'death', 'nonfinite'])
     args = ap.parse_args()
     pn, vt = load_reference()
     if args.only in (None, 'kernels'):
@@ -503,6 +571,8 @@ def main():
         gen_ros_replay(pn, vt, args.out)
     if args.only in (None, 'death'):
         gen_death(pn, args.out)
+    if args.only in (None, 'nonfinite'):
+        gen_nonfinite(pn, args.out)
     print('golden vectors written to', args.out)
 
 

@@ -3,7 +3,7 @@ the reference itself (tests/golden/gen_golden.py) must be reproduced exactly."""
 import numpy as np
 import pytest
 
-from conftest import dense_state, load_golden
+from conftest import dense_state, load_golden, nonfinite_state
 from oracle import posecell as P
 from oracle import view_templates as V
 
@@ -68,6 +68,30 @@ def test_network_death_bit_exact(name):
         assert np.array_equal(net.posecells, dense_state(case, s)), (name, s)
         if kill <= s < revive:
             assert not net.posecells.any() and m == (0, 0, 0)
+
+
+def test_nonfinite_odometry_bit_exact():
+    """pc_nonfinite (made by the reference, with Python 2's floor of a non-finite theta
+    origin, tests/golden/gen_golden.py): a NaN or -inf vrot leaves an all-NaN volume for
+    good with peak (0, 0, 0); a NaN or inf vtrans raises ValueError after steps 1-4 of
+    its update, whose state the oracle reproduces bit for bit."""
+    case = load_golden('pc_nonfinite')
+    shape, loc = tuple(case['shape']), tuple(case['inject'])
+    for i, vr in enumerate(case['vrot']):
+        net = P.PoseCellOracle(shape)
+        net.inject(1, loc)
+        for s, v in enumerate(case['vrot_odom_other']):
+            m = net.update((v[0], vr) if s == 1 else tuple(v))
+            assert m == tuple(case['vrot_max_pc'][i][s]), (i, s)
+            assert bool(np.isnan(net.posecells).all()) == bool(case['vrot_all_nan'][i][s]), (i, s)
+    for i, vt in enumerate(case['vtrans']):
+        net = P.PoseCellOracle(shape)
+        net.inject(1, loc)
+        assert net.update((0.2, 0.01)) == tuple(case['vtrans_pre_max_pc'][i])
+        assert str(case['vtrans_raised'][i]) == 'ValueError'
+        with pytest.raises(ValueError):
+            net.update((vt, 0.0))
+        assert np.array_equal(net.posecells, nonfinite_state(case, i)), i
 
 
 def test_keyerror_parity():

@@ -590,6 +590,34 @@ def test_large_grid_wide_shifts_vs_c_oracle(pcn, precision, tol):
     assert np.abs(net.posecells - ref.posecells).max() < tol
 
 
+@pytest.mark.parametrize('form,precision', [('', 'float32'), ('', 'float64'), ('cols', 'float32')])
+def test_nonfinite_odometry_vs_reference_fixture(pcn, monkeypatch, form, precision):
+    """pc_nonfinite, made by the reference itself (tests/golden/gen_golden.py): NaN / -inf
+    vrot leaves an all-NaN volume for good, peak (0, 0, 0) per step; NaN / inf vtrans
+    raises ValueError after steps 1-4, whose state matches the reference's (32 x 32 x 18:
+    the halo form by default since round 6, rows at float64, the column form)."""
+    from conftest import nonfinite_state
+    monkeypatch.setenv('RS_PC_FORM', form)
+    case = load_golden('pc_nonfinite')
+    shape, loc = tuple(int(x) for x in case['shape']), tuple(int(x) for x in case['inject'])
+    tol = F32_TOL if precision == 'float32' else F64_TOL
+    for i, vr in enumerate(case['vrot']):
+        net = pcn(shape, precision=precision)
+        assert not form or net.step_form() == form
+        net.inject(1, loc)
+        for st, v in enumerate(case['vrot_odom_other']):
+            m = net.update((v[0], vr) if st == 1 else tuple(v))
+            assert m == tuple(case['vrot_max_pc'][i][st]), (i, st)
+            assert bool(np.isnan(net.posecells).all()) == bool(case['vrot_all_nan'][i][st]), (i, st)
+    for i, vt in enumerate(case['vtrans']):
+        net = pcn(shape, precision=precision)
+        net.inject(1, loc)
+        assert net.update((0.2, 0.01)) == tuple(case['vtrans_pre_max_pc'][i])
+        with pytest.raises(ValueError):
+            net.update((vt, 0.0))
+        assert np.abs(net.posecells - nonfinite_state(case, i)).max() < tol, i
+
+
 @pytest.mark.parametrize('form,precision', [('', 'float32'), ('', 'float64'), ('halo', 'float32'),
                                             ('cols', 'float32')])
 def test_nonfinite_odometry_like_reference(pcn, monkeypatch, form, precision):
