@@ -2314,8 +2314,8 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
     unsigned long long bk = 0ull;
     const bool want_key = slot_prev != nullptr;
     PC_STAMP(11, 0);
-    // a thread per union cell (theta extents other than HF_TH; at HF_TH a union spanning
-    // a whole period, or one larger than the LDS-DMA image)
+    // a thread per union cell (theta extents other than HF_TH; at HF_TH a union larger
+    // than the LDS-DMA image)
     auto cell_passes = [&]() __attribute__((always_inline)) {
         // a union spanning a whole period (the windows wrap inside it), or one larger
         // than the LDS-DMA image (columns from memory): thread c takes union cell c's
@@ -2377,7 +2377,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     };
     if constexpr (TH == HF_TH) {
-      if (dma && !cwrap) {
+      if (dma) {
         // the common case, read straight from the union image [cell][layer]: wave w < 8
         // takes window rows 4(w&3) .. +3 (a lane per window cell) through the layers
         // [18(w>>2), +18).  Layer j's window cell (rx, ry) is union cell (rx + sx_j,
@@ -2406,14 +2406,24 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             const int rx = 4 * (wave & 3) + (lane >> 4), ry = lane & 15;
             const int loff = (lsx * UH + lsy) * TH;   // lane L: layer L's window place in the union
             const int cbase = (rx * UH + ry) * TH;
-            auto run = [&](auto hh) __attribute__((always_inline)) {
+            auto run = [&](auto hh, auto wc) __attribute__((always_inline)) {
                 constexpr int J0 = decltype(hh)::value * JH;
+                constexpr bool WRAP = decltype(wc)::value;
                 // quads kq = 0 .. NQ-1 hold layers 4 (QB + kq) .. +3 (mod TH) of the current cell
                 constexpr int QB = (J0 - HALF + 4 * TH) / 4 - TH, NQ = (J0 + JH - 1 + HALF - 4 * QB) / 4 + 1;
                 co_f4 qd[NQ];
                 hf_f2* dst = s_tw + J0 * HF_WJ + (rx * HF_WP + ry);
+                // a union spanning a whole period (cwrap: 16 + the shifts' spread exceeds X
+                // or Y, so the union is the period): window cell (rx, ry) of layer j is
+                // union cell ((rx + sx_j) mod UW, (ry + sy_j) mod UH); else no wrap occurs
+                auto colof = [&](int j) __attribute__((always_inline)) {
+                    int ux = rx + __builtin_amdgcn_readlane(lsx, j), uy = ry + __builtin_amdgcn_readlane(lsy, j);
+                    ux -= ux >= UW ? UW : 0;
+                    uy -= uy >= UH ? UH : 0;
+                    return s_b + (ux * UH + uy) * TH;
+                };
                 int prev = __builtin_amdgcn_readlane(loff, J0);
-                const float* col = s_b + cbase + prev;
+                const float* col = WRAP ? colof(J0) : s_b + cbase + prev;
                 auto ld = [&](int kq) {
                     qd[kq] = *reinterpret_cast<const co_f4*>(col + ((4 * (QB + kq) + 4 * TH) % TH)) * nrm.r;
                 };
@@ -2441,7 +2451,7 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                         if (e % 4 == 0 && e / 4 < NQ) ld(e / 4);
                     } else {
                         prev = o;
-                        col = s_b + cbase + o;
+                        col = WRAP ? colof(J0 + jj) : s_b + cbase + o;
                         ld_span(e0, e0 + 2 * HALF + PF);
                     }
                 };
@@ -2471,8 +2481,14 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                     }
                 }
             };
-            if (wave < 4) run(std::integral_constant<int, 0>{});
-            else run(std::integral_constant<int, 1>{});
+            // (separate code for a wrapped union, so the common case keeps its registers)
+            if (!cwrap) {
+                if (wave < 4) run(std::integral_constant<int, 0>{}, std::false_type{});
+                else run(std::integral_constant<int, 1>{}, std::false_type{});
+            } else {
+                if (wave < 4) run(std::integral_constant<int, 0>{}, std::true_type{});
+                else run(std::integral_constant<int, 1>{}, std::true_type{});
+            }
         } else if (want_key) {
             // wave 8: the argmax of the state entering the step over the own tile (lane:
             // cell lane & 15, quads lane >> 4 + 4 m)

@@ -161,6 +161,35 @@ def test_uniform_large_shift_own_tile_outside_union(halo):
     assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
 
 
+def test_wrapped_union_per_layer_shifts(halo):
+    """Per-layer shifts whose spread makes the union span a whole period (16 + spread
+    > 21): the 36-layer theta pass then maps window cells to union cells modulo the
+    period.  Shifts change from layer to layer (each change reloads a column) and
+    wrap in x only, in y only and in both."""
+    shape = (21, 21, 36)
+    net = halo(shape)
+    ref = P.PoseCellOracle(shape)
+    for x in (net, ref):
+        x.inject(1, (10, 10, 18))
+    table = net._table
+    zf = np.ascontiguousarray(P.dog_offset_1d(0), dtype=np.float64)
+    j = np.arange(36)
+    cases = [((j % 7) - 3, 3 - (j * 5) % 9),        # both
+             ((j // 4) % 7 - 3, np.full(36, 1)),     # x only
+             (np.zeros(36, int), (j * 3) % 8 - 4),   # y only
+             ((j % 2) * 8 - 4, (j % 3) * 4 - 4)]     # every layer a new shift
+    for s, (sx, sy) in enumerate(cases * 2):
+        ox = np.ascontiguousarray(sx, dtype=np.int32)
+        oy = np.ascontiguousarray(sy, dtype=np.int32)
+        rows = np.full(36, net.filter_table.index[(0, 0)], dtype=np.int32)
+        want = _oracle_step_with_control(ref, ox, oy, rows, zf, table)
+        st = net._update(net._h, ox.ctypes.data, oy.ctypes.data, rows.ctypes.data, zf.ctypes.data,
+                         net._out3_addr)
+        assert st == 0
+        assert tuple(int(v) for v in net._out3) == want, s
+    assert np.abs(net.posecells - ref.posecells).max() < F32_TOL
+
+
 def test_poisoned_scratch_first_updates_vs_c_oracle(halo):
     from oracle import c_oracle as C
     from pyratslam_amd import _lib
