@@ -2321,10 +2321,14 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         // than the LDS-DMA image (columns from memory): thread c takes union cell c's
         // column, scales it, forms all TH theta-pass outputs in registers and stores
         // those of the windows holding the cell (a lane outside a window stores into its
-        // own dump slot, so the layers' chains interleave with no exec changes)
+        // own dump slot, a select rather than a branch, so the layers' FMA chains share
+        // one basic block and interleave).  The own tile's keys: wave 8 when the union
+        // is in LDS (below; HF_UMAX < 512, so wave 8 holds no union cell), else here.
+        static_assert(HF_UMAX <= 8 * 64, "wave 8 takes no union cell");
         auto cell_pass = [&](int c, auto wrap_c) __attribute__((always_inline)) {
             constexpr bool WRAP = decltype(wrap_c)::value;
-            const int ui = c / UH, vi = c - ui * UH;
+            const int ui = (int)__umulhi((unsigned)c, muh), vi = c - ui * UH;   // c / UH (hf_magic)
+            const int cw = ui * HF_WP + vi, dump = TH * HF_WJ + tid;
             int gr = ux0 + ui, gc = uy0 + vi;
             gr -= gr >= X ? X : 0;
             gc -= gc >= Y ? Y : 0;
@@ -2345,27 +2349,35 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             if (dma) rd(s_b + c * TH);
             else rd(U + ((size_t)gr * Y + gc) * TH);
             nrm(p);
-            if (want_key && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
+            if (want_key && !dma && (unsigned)(gr - x0) < (unsigned)tw && (unsigned)(gc - y0) < (unsigned)tht) {
                 const unsigned lin0 = ((unsigned)gr * Y + gc) * TH;
 #pragma unroll
                 for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
             }
-#pragma unroll
-            for (int j = 0; j < TH; ++j) {
+            auto store = [&](int j, hf_f2 eg) __attribute__((always_inline)) {
                 const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
-                hf_f2 eg = {0.f, 0.f};
-#pragma unroll
-                for (int t = 0; t < FL; ++t) eg += gei[t] * p[(j + t + TH - HALF) % TH];
                 if constexpr (WRAP) {
                     int rx = ui - sxj, ry = vi - syj;
                     rx += rx < 0 ? UW : 0;
                     ry += ry < 0 ? UH : 0;
-                    if ((unsigned)rx < (unsigned)HF_W && (unsigned)ry < (unsigned)HF_W)
-                        s_tw[j * HF_WJ + rx * HF_WP + ry] = eg;
+                    const int a = j * HF_WJ + (int)__umul24((unsigned)rx, (unsigned)HF_WP) + ry;
+                    s_tw[max((unsigned)rx, (unsigned)ry) < (unsigned)HF_W ? a : dump] = eg;
                 } else {
-                    const bool in = max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W;
-                    s_tw[in ? j * HF_WJ + (ui - sxj) * HF_WP + (vi - syj) : TH * HF_WJ + tid] = eg;
+                    const int a = j * HF_WJ + cw - (sxj * HF_WP + syj);   // the shift's part is scalar
+                    s_tw[max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W ? a : dump] = eg;
                 }
+            };
+            // layers in pairs: two independent FMA chains interleaved
+#pragma unroll
+            for (int j = 0; j < TH; j += 2) {
+                hf_f2 ea = {0.f, 0.f}, eb = {0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < FL; ++t) {
+                    ea += gei[t] * p[(j + t + TH - HALF) % TH];
+                    eb += gei[t] * p[(j + 1 + t + TH - HALF) % TH];
+                }
+                store(j, ea);
+                store(j + 1, eb);
             }
         };
         if (cwrap) {
@@ -2511,6 +2523,19 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
       }
     } else {
         cell_passes();
+        if (dma && want_key && wave == 8) {
+            // the own tile's keys from the image, off the cell-pass waves (lane: cell
+            // lane & 15, layers lane >> 4 + 4 m), scaled as cell_pass scales
+            const int i = (lane & 15) >> 2, jc = lane & 3;
+            int cu = co_wrap(2 * HALF - cux, X) + i, cv = co_wrap(2 * HALF - cuy, Y) + jc;
+            cu -= cu >= X ? X : 0;
+            cv -= cv >= Y ? Y : 0;
+            if (i < tw && jc < tht && cu < UW && cv < UH) {
+                const unsigned lin0 = ((unsigned)(x0 + i) * Y + (y0 + jc)) * TH;
+                const float* src = s_b + (cu * UH + cv) * TH;
+                for (int q = lane >> 4; q < TH; q += 4) bk = max(bk, argmax_key(nrm(src[q]), lin0 + q));
+            }
+        }
     }
     PC_STAMP(11, 1);
     PC_STAMPW(12);
