@@ -2329,6 +2329,13 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
             constexpr bool WRAP = decltype(wrap_c)::value;
             const int ui = (int)__umulhi((unsigned)c, muh), vi = c - ui * UH;   // c / UH (hf_magic)
             const int cw = ui * HF_WP + vi, dump = TH * HF_WJ + tid;
+            // (no wrap) lane L: layer L's window start as packed 16-bit (x, y), and the
+            // byte offset of its window cell (0, 0) in layer 0's window image; the lane's
+            // cell, packed and in bytes (pinned: one subtraction per layer each)
+            const int lsp = (lsx << 16) + lsy, lso8 = 8 * (lsx * HF_WP + lsy - lane * HF_WJ);
+            int uvp = (ui << 16) + vi, cw8 = 8 * cw;
+            asm volatile("" : "+v"(uvp), "+v"(cw8));
+            const int dump8 = 8 * dump;
             int gr = ux0 + ui, gc = uy0 + vi;
             gr -= gr >= X ? X : 0;
             gc -= gc >= Y ? Y : 0;
@@ -2355,16 +2362,21 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
                 for (int q = 0; q < TH; ++q) bk = max(bk, argmax_key(p[q], lin0 + q));
             }
             auto store = [&](int j, hf_f2 eg) __attribute__((always_inline)) {
-                const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
                 if constexpr (WRAP) {
+                    const int sxj = __builtin_amdgcn_readlane(lsx, j), syj = __builtin_amdgcn_readlane(lsy, j);
                     int rx = ui - sxj, ry = vi - syj;
                     rx += rx < 0 ? UW : 0;
                     ry += ry < 0 ? UH : 0;
                     const int a = j * HF_WJ + (int)__umul24((unsigned)rx, (unsigned)HF_WP) + ry;
                     s_tw[max((unsigned)rx, (unsigned)ry) < (unsigned)HF_W ? a : dump] = eg;
                 } else {
-                    const int a = j * HF_WJ + cw - (sxj * HF_WP + syj);   // the shift's part is scalar
-                    s_tw[max((unsigned)(ui - sxj), (unsigned)(vi - syj)) < (unsigned)HF_W ? a : dump] = eg;
+                    // in the window: both 16-bit fields of the packed difference in [0, 16)
+                    // (a negative y part borrows into bits 4-15 of the low field);
+                    // |coordinates| < 2^15
+                    static_assert(HF_W == 16, "the packed window test");
+                    const int d = uvp - __builtin_amdgcn_readlane(lsp, j);
+                    const int a8 = cw8 - __builtin_amdgcn_readlane(lso8, j);
+                    *reinterpret_cast<hf_f2*>(reinterpret_cast<char*>(s_tw) + ((d & 0xFFF0FFF0) == 0 ? a8 : dump8)) = eg;
                 }
             };
             // layers in pairs: two independent FMA chains interleaved
@@ -2592,7 +2604,19 @@ __global__ __launch_bounds__(HF_NT) void pc_step_halo(
         }
     };
     static_assert(HF_W == 16 && HF_Q == 10 && HF_NW == 9, "phase 3's task split");
-    if constexpr (TH != 36) {
+    if constexpr (TH == 18) {
+        // waves 0-3 take layers 0-15 whole, one wave per SIMD; layers 16-17 go in 4-, 3-
+        // and 3-output pieces to waves 5, 6, 7 (SIMDs 1-3): 288 whole tasks on 5 waves
+        // put two on SIMD 0
+        using I = std::integral_constant<int, 0>;
+        if (wave < 4) ytask(tid >> 4, tid & 15, I{}, std::integral_constant<int, HF_Q>{});
+        const int jr = 16 + ((lane >> 4) & 1), rr = lane & 15;
+        if (lane < 32) {
+            if (wave == 5) ytask(jr, rr, I{}, std::integral_constant<int, 4>{});
+            else if (wave == 6) ytask(jr, rr, std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
+            else if (wave == 7) ytask(jr, rr, std::integral_constant<int, 7>{}, std::integral_constant<int, 3>{});
+        }
+    } else if constexpr (TH != 36) {
         for (int t = tid; t < TH * HF_W; t += HF_NT)
             ytask(t >> 4, t & 15, std::integral_constant<int, 0>{}, std::integral_constant<int, HF_Q>{});
     } else {
